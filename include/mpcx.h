@@ -1,0 +1,162 @@
+/* mpcx.h -- C ABI of the MI355X-native batched multiple-shooting MPC solver.
+ *
+ * The drop-in boundary for the hot path of gabrielhaj/mpc-verde.  Every entry
+ * point replaces one call site of the reference's CasADi boundary (paths
+ * relative to the reference repository):
+ *
+ *   mpcx_create         ca.nlpsol('solver', 'ipopt', prob, opts)
+ *                         Casadi/multiple_shooting_casadi.py:181-197
+ *                         (problem = the NLP built at :68-178; options :188-196)
+ *   mpcx_solve_batch    sol = solver(x0=, lbx=, ubx=, lbg=, ubg=, p=)
+ *                         Casadi/multiple_shooting_casadi.py:235-242, batched
+ *                         over B independent parameter vectors p
+ *   mpcx_plant_step     state_init = F(args['p'], u[:, 0])[0]
+ *                         Casadi/multiple_shooting_casadi.py:273 (F built at :98-114)
+ *   mpcx_rk4_sens       the function + derivative evaluations IPOPT requests from
+ *                         CasADi inside solver() (F and its AD, :157 / :197):
+ *                         kernel-level entry of the RK4 + Jacobian sweep
+ *   mpcx_destroy        (Python garbage collection of the solver object)
+ *   mpcx_last_error     (CasADi raises RuntimeError; here: message of the last
+ *                         failing call on this thread)
+ *
+ * Conventions.  All arithmetic is IEEE fp64.  Pointers named d_* are device
+ * pointers (hipMalloc'ed or torch CUDA tensors); everything else is host memory.
+ * Functions return 0 on success and a negative mpcx_err code on error.  Host
+ * calls are synchronous.  A handle is owned by one host thread at a time.
+ *
+ * Decision-vector layout = the reference's interleaved w (:128-170):
+ *   w = [X_0(nx) | U_0(nu) X_1(nx) | ... | U_{N-1}(nu) X_N(nx)],  n_w = nx + N(nu+nx)
+ * Constraint layout (:131,:172-175), all equalities (lbg = ubg = 0):
+ *   g = [P[:nx] - X_0 ; F(X_k,U_k).xf - X_{k+1}  (k = 0..N-1)],  n_g = nx (N+1)
+ */
+#ifndef MPCX_H_
+#define MPCX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mpcx_handle mpcx_handle;
+
+enum mpcx_model {
+  MPCX_MODEL_UNICYCLE = 1 /* x=(x,y,theta), u=(v,omega): Casadi/multiple_shooting_casadi.py:68-72 */
+};
+
+enum mpcx_cost {
+  /* J = sum_k RK4 quadrature of L over [t_k, t_k+T] (Casadi/multiple_shooting_casadi.py:98-113) */
+  MPCX_COST_QUADRATURE = 0,
+  /* J = sum_k l(x_k, u_k, p_k) at the shooting nodes (mpctools nmpc;
+     Trajectory Tracking/Trajectory_tracking.py:57-61) */
+  MPCX_COST_NODE = 1
+};
+
+enum mpcx_param_layout {
+  /* p = [x0 (nx); x_ref (nx)]  (n_p = 2 nx, Casadi/multiple_shooting_casadi.py:74,228-231) */
+  MPCX_P_X0_XREF = 0,
+  /* p = [x0 (nx); (x_ref_k, u_ref_k) for k = 0..N-1]  (n_p = nx + N (nx+nu);
+     Trajectory Tracking/Trajectory_tracking.py:84-97,105-106) */
+  MPCX_P_X0_STAGEREF = 1
+};
+
+enum mpcx_status {
+  MPCX_CONVERGED = 0,   /* optimality error <= tol (IPOPT "Solve_Succeeded") */
+  MPCX_ACCEPTABLE = 1,  /* reserved */
+  MPCX_MAX_ITER = 2,    /* iteration limit reached */
+  MPCX_FAILED = 3       /* line search / inertia correction failed, or non-finite values */
+};
+
+enum mpcx_err {
+  MPCX_OK = 0,
+  MPCX_EINVAL = -1,  /* bad argument (message via mpcx_last_error) */
+  MPCX_EHIP = -2,    /* HIP runtime error */
+  MPCX_ENOMEM = -3
+};
+
+typedef struct mpcx_spec {
+  int32_t model;        /* mpcx_model */
+  int32_t cost;         /* mpcx_cost */
+  int32_t param_layout; /* mpcx_param_layout */
+  int32_t N;            /* horizon (intervals), 1..63 */
+  int32_t M;            /* RK4 substeps per interval (M at :101; mpctools M at Trajectory_tracking.py:51) */
+  int32_t max_iter;     /* IPOPT max_iter (:190) */
+  int32_t device;       /* HIP device ordinal */
+  int32_t reserved;
+  double T;             /* sampling time (:31) */
+  double tol;           /* IPOPT tol (default 1e-8) */
+  double Q[8];          /* diagonal state weights (:78-83) */
+  double R[8];          /* diagonal control weights (:81-84) */
+  double lbu[8], ubu[8];/* control bounds (:42-45) */
+  double lbx[8], ubx[8];/* state bounds (+-1e20 = free; Trajectory_tracking.py:64-67) */
+} mpcx_spec;
+
+/* Fill *s with the reference's constants for model/cost at horizon N
+   (unicycle point-to-point: T=0.2, M=4, Q=diag(1,5,0.1), R=diag(0.5,0.05),
+   |v|<=1, |omega|<=pi/4, max_iter=2000, tol=1e-8). */
+int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N);
+
+int mpcx_create(const mpcx_spec* s, mpcx_handle** h);
+void mpcx_destroy(mpcx_handle* h);
+const char* mpcx_last_error(void);
+
+/* n_w, n_g, n_p of the NLP described by the handle. */
+int mpcx_dims(const mpcx_handle* h, int32_t* n_w, int32_t* n_g, int32_t* n_p);
+
+/* Batched NLP solve (host pointers, synchronous).
+ *   P      B x n_p parameters (layout per spec.param_layout)
+ *   w0     B x n_w initial guesses, or NULL = cold start (X_k = x0, U_k = 0,
+ *          the reference's repmat(state_init) / zeros initialisation, :212-213)
+ *   lbw/ubw n_w bound vectors shared by the batch, or NULL = spec bounds
+ *          (the reference's lbx/ubx, :199-206; X_0 is always free: it is
+ *          pinned by the lifted constraint g_0)
+ *   w_out  B x n_w optimal decision vectors (interleaved reference layout)
+ *   f_out  B objective values, or NULL
+ *   g_out  B x n_g constraint values at w_out, or NULL
+ *   lam_g  B x n_g constraint multipliers (CasADi sign convention), or NULL
+ *   status B mpcx_status codes, or NULL
+ *   iters  B iteration counts, or NULL                                        */
+int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w0, const double* lbw,
+                     const double* ubw, double* w_out, double* f_out, double* g_out, double* lam_g,
+                     int32_t* status, int32_t* iters);
+
+/* Device-pointer variant: no host synchronisation; all work is enqueued on
+   `stream` (a hipStream_t, NULL = default stream).  d_w0 may be NULL (cold). */
+int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const double* d_w0, double* d_w_out,
+                         double* d_f_out, double* d_lam_g, int32_t* d_status, int32_t* d_iters, void* stream);
+
+/* Plant / integrator F (host): xf = F(x0, u).xf, qf = F(x0, u).qf for B
+   instances; P as in mpcx_solve_batch (only x0 and the stage-0 reference are
+   read), u B x nu.  qf may be NULL. */
+int mpcx_plant_step(mpcx_handle* h, int32_t B, const double* P, const double* u, double* xf, double* qf);
+
+/* Receding-horizon update on the device (one closed-loop step of
+   Casadi/multiple_shooting_casadi.py:271-287): x0 <- F(x0, u_0*) in d_P, and
+   d_w0_next = the optimal w shifted by one interval (last interval repeated). */
+int mpcx_shift_dev(mpcx_handle* h, int32_t B, double* d_P, const double* d_w, double* d_w0_next, void* stream);
+
+/* RK4 + Jacobian sweep over B x N shooting intervals (host pointers).
+ *   w      B x n_w decision vectors (interleaved layout)
+ *   P      B x n_p parameters
+ * Outputs, per instance b and interval k (row-major, k fastest after b):
+ *   c      B x N x nx   defects F(X_k,U_k).xf - X_{k+1}
+ *   q      B x N        F(X_k,U_k).qf
+ *   A      B x N x nx x nx   dF.xf/dX_k
+ *   Bm     B x N x nx x nu   dF.xf/dU_k
+ *   gq     B x N x (nx+nu)   dF.qf/d(X_k,U_k)                               */
+int mpcx_rk4_sens(mpcx_handle* h, int32_t B, const double* w, const double* P, double* c, double* q, double* A,
+                  double* Bm, double* gq);
+
+/* Device variant of the sweep on structure-of-arrays buffers (the layout the
+   kernel streams from HBM):
+ *   d_X  (N+1) x nx x B,  d_U  N x nu x B,  d_xr nx x B      (inputs)
+ *   d_c  N x nx x B, d_q N x B, d_A N x nx*nx x B, d_Bm N x nx*nu x B,
+ *   d_gq N x (nx+nu) x B                                      (outputs)       */
+int mpcx_rk4_sens_dev(mpcx_handle* h, int32_t B, const double* d_X, const double* d_U, const double* d_xr,
+                      double* d_c, double* d_q, double* d_A, double* d_Bm, double* d_gq, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MPCX_H_ */

@@ -1,0 +1,408 @@
+// capi.cpp -- extern "C" boundary of libmpcx.so (declared in include/mpcx.h).
+//
+// Host-pointer entry points stage inputs into a device workspace owned by the
+// handle (grown on demand, never freed inside a solve), launch on the handle's
+// stream and copy results back; *_dev entry points only enqueue work.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mpcx.h"
+#include "solver.h"
+
+
+struct mpcx_handle {
+  mpcx_spec spec;
+  int nw, ng, np;
+  hipStream_t stream = nullptr;
+  double* d_lbw = nullptr;  // spec bounds
+  double* d_ubw = nullptr;
+  double* d_lbw_call = nullptr;  // per-call bounds
+  double* d_ubw_call = nullptr;
+  // workspace (grown on demand)
+  size_t cap_B = 0;
+  double *d_P = nullptr, *d_w0 = nullptr, *d_w = nullptr, *d_f = nullptr, *d_lam = nullptr;
+  int32_t *d_status = nullptr, *d_iters = nullptr;
+  size_t cap_sweep = 0;
+  double* d_sweep = nullptr;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+int hipfail(hipError_t e, const char* where) {
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return MPCX_EHIP;
+}
+#define HIPCHK(expr)                                   \
+  do {                                                 \
+    hipError_t e_ = (expr);                            \
+    if (e_ != hipSuccess) return hipfail(e_, #expr);   \
+  } while (0)
+
+mpcx::StageParams stage_params(const mpcx_spec& s) {
+  mpcx::StageParams sp;
+  sp.T = s.T;
+  sp.M = s.M;
+  sp.h = s.T / s.M;
+  sp.cost = s.cost;
+  for (int i = 0; i < 3; ++i) sp.Q[i] = s.Q[i];
+  for (int i = 0; i < 2; ++i) sp.R[i] = s.R[i];
+  return sp;
+}
+
+void spec_bounds(const mpcx_spec& s, std::vector<double>& lb, std::vector<double>& ub) {
+  const int N = s.N, nw = 3 + 5 * N;
+  lb.assign(nw, -1e20);
+  ub.assign(nw, 1e20);
+  for (int k = 0; k < N; ++k) {
+    for (int i = 0; i < 2; ++i) {
+      lb[3 + 5 * k + i] = s.lbu[i];
+      ub[3 + 5 * k + i] = s.ubu[i];
+    }
+    for (int i = 0; i < 3; ++i) {
+      lb[5 + 5 * k + i] = s.lbx[i];
+      ub[5 + 5 * k + i] = s.ubx[i];
+    }
+  }
+}
+
+int ensure(mpcx_handle* h, size_t B) {
+  if (B <= h->cap_B) return 0;
+  size_t nb = B < 256 ? 256 : B;
+  (void)hipFree(h->d_P);
+  (void)hipFree(h->d_w0);
+  (void)hipFree(h->d_w);
+  (void)hipFree(h->d_f);
+  (void)hipFree(h->d_lam);
+  (void)hipFree(h->d_status);
+  (void)hipFree(h->d_iters);
+  h->cap_B = 0;
+  HIPCHK(hipMalloc(&h->d_P, nb * h->np * sizeof(double)));
+  HIPCHK(hipMalloc(&h->d_w0, nb * h->nw * sizeof(double)));
+  HIPCHK(hipMalloc(&h->d_w, nb * h->nw * sizeof(double)));
+  HIPCHK(hipMalloc(&h->d_f, nb * sizeof(double)));
+  HIPCHK(hipMalloc(&h->d_lam, nb * h->ng * sizeof(double)));
+  HIPCHK(hipMalloc(&h->d_status, nb * sizeof(int32_t)));
+  HIPCHK(hipMalloc(&h->d_iters, nb * sizeof(int32_t)));
+  h->cap_B = nb;
+  return 0;
+}
+
+int check_bounds_vec(const mpcx_handle* h, const double* lbw, const double* ubw) {
+  if (!lbw && !ubw) return 0;
+  for (int i = 0; i < h->nw; ++i) {
+    const double l = lbw ? lbw[i] : -1e20, u = ubw ? ubw[i] : 1e20;
+    if (std::isnan(l) || std::isnan(u) || l > u) return fail(MPCX_EINVAL, "lbw/ubw: NaN or lb > ub at index " + std::to_string(i));
+    if (l == u && l > -1e19) return fail(MPCX_EINVAL, "lbw == ubw (fixed variable) is not supported, index " + std::to_string(i));
+  }
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
+const char* mpcx_last_error(void) { return g_err.c_str(); }
+
+int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N) {
+  if (!s) return fail(MPCX_EINVAL, "null spec");
+  if (model != MPCX_MODEL_UNICYCLE) return fail(MPCX_EINVAL, "unknown model");
+  std::memset(s, 0, sizeof *s);
+  // Casadi/multiple_shooting_casadi.py:30-45, 78-84, 101, 188-196
+  s->model = model;
+  s->cost = MPCX_COST_QUADRATURE;
+  s->param_layout = MPCX_P_X0_XREF;
+  s->N = N;
+  s->M = 4;
+  s->max_iter = 2000;
+  s->device = 0;
+  s->T = 0.2;
+  s->tol = 1e-8;
+  s->Q[0] = 1.0; s->Q[1] = 5.0; s->Q[2] = 0.1;
+  s->R[0] = 0.5; s->R[1] = 0.05;
+  s->lbu[0] = -1.0; s->ubu[0] = 1.0;
+  s->lbu[1] = -M_PI / 4; s->ubu[1] = M_PI / 4;
+  for (int i = 0; i < 3; ++i) {
+    s->lbx[i] = -1e20;
+    s->ubx[i] = 1e20;
+  }
+  return 0;
+}
+
+int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
+  if (!s || !out) return fail(MPCX_EINVAL, "null argument");
+  if (s->model != MPCX_MODEL_UNICYCLE) return fail(MPCX_EINVAL, "unknown model");
+  if (s->N < 1 || s->N > 63) return fail(MPCX_EINVAL, "N must be in [1, 63]");
+  if (s->M < 1 || s->M > 64) return fail(MPCX_EINVAL, "M must be in [1, 64]");
+  if (!(s->T > 0)) return fail(MPCX_EINVAL, "T must be > 0");
+  if (s->cost != MPCX_COST_QUADRATURE && s->cost != MPCX_COST_NODE) return fail(MPCX_EINVAL, "unknown cost");
+  if (s->param_layout != MPCX_P_X0_XREF && s->param_layout != MPCX_P_X0_STAGEREF)
+    return fail(MPCX_EINVAL, "unknown param_layout");
+  if (s->max_iter < 0) return fail(MPCX_EINVAL, "max_iter < 0");
+  if (!(s->tol > 0)) return fail(MPCX_EINVAL, "tol must be > 0");
+  for (int i = 0; i < 2; ++i)
+    if (!(s->lbu[i] < s->ubu[i])) return fail(MPCX_EINVAL, "lbu must be < ubu");
+  for (int i = 0; i < 3; ++i)
+    if (!(s->lbx[i] < s->ubx[i])) return fail(MPCX_EINVAL, "lbx must be < ubx");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) return fail(MPCX_EHIP, "no HIP device available");
+  if (s->device < 0 || s->device >= ndev) return fail(MPCX_EINVAL, "device ordinal out of range");
+  HIPCHK(hipSetDevice(s->device));
+  mpcx_handle* h = new mpcx_handle();
+  h->spec = *s;
+  h->nw = 3 + 5 * s->N;
+  h->ng = 3 * (s->N + 1);
+  h->np = s->param_layout == MPCX_P_X0_XREF ? 6 : 3 + 5 * s->N;
+  std::vector<double> lb, ub;
+  spec_bounds(*s, lb, ub);
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&h->d_lbw, h->nw * sizeof(double)) != hipSuccess ||
+      hipMalloc(&h->d_ubw, h->nw * sizeof(double)) != hipSuccess ||
+      hipMalloc(&h->d_lbw_call, h->nw * sizeof(double)) != hipSuccess ||
+      hipMalloc(&h->d_ubw_call, h->nw * sizeof(double)) != hipSuccess ||
+      hipMemcpy(h->d_lbw, lb.data(), h->nw * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->d_ubw, ub.data(), h->nw * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+    mpcx_destroy(h);
+    return fail(MPCX_EHIP, "device allocation failed in mpcx_create");
+  }
+  *out = h;
+  return 0;
+}
+
+void mpcx_destroy(mpcx_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->spec.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  (void)hipFree(h->d_lbw);
+  (void)hipFree(h->d_ubw);
+  (void)hipFree(h->d_lbw_call);
+  (void)hipFree(h->d_ubw_call);
+  (void)hipFree(h->d_P);
+  (void)hipFree(h->d_w0);
+  (void)hipFree(h->d_w);
+  (void)hipFree(h->d_f);
+  (void)hipFree(h->d_lam);
+  (void)hipFree(h->d_status);
+  (void)hipFree(h->d_iters);
+  (void)hipFree(h->d_sweep);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int mpcx_dims(const mpcx_handle* h, int32_t* n_w, int32_t* n_g, int32_t* n_p) {
+  if (!h) return fail(MPCX_EINVAL, "null handle");
+  if (n_w) *n_w = h->nw;
+  if (n_g) *n_g = h->ng;
+  if (n_p) *n_p = h->np;
+  return 0;
+}
+
+static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, const double* w0, const double* lbw,
+                                 const double* ubw, double* w, double* f, double* lam, int32_t* st, int32_t* it) {
+  mpcx::SolveArgs a;
+  a.B = B;
+  a.N = h->spec.N;
+  a.max_iter = h->spec.max_iter;
+  a.p_layout = h->spec.param_layout;
+  a.p_stride = h->np;
+  a.tol = h->spec.tol;
+  a.sp = stage_params(h->spec);
+  a.P = P;
+  a.w0 = w0;
+  a.lbw = lbw;
+  a.ubw = ubw;
+  a.w_out = w;
+  a.f_out = f;
+  a.lam_out = lam;
+  a.status = st;
+  a.iters = it;
+  return a;
+}
+
+int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const double* d_w0, double* d_w_out,
+                         double* d_f_out, double* d_lam_g, int32_t* d_status, int32_t* d_iters, void* stream) {
+  if (!h || !d_P || !d_w_out) return fail(MPCX_EINVAL, "null argument");
+  if (B < 0) return fail(MPCX_EINVAL, "B < 0");
+  if (B == 0) return 0;
+  HIPCHK(hipSetDevice(h->spec.device));
+  mpcx::SolveArgs a = make_args(h, B, d_P, d_w0, h->d_lbw, h->d_ubw, d_w_out, d_f_out, d_lam_g, d_status, d_iters);
+  HIPCHK(mpcx::launch_solve(a, (hipStream_t)stream));
+  return 0;
+}
+
+int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w0, const double* lbw,
+                     const double* ubw, double* w_out, double* f_out, double* g_out, double* lam_g, int32_t* status,
+                     int32_t* iters) {
+  if (!h || !P || !w_out) return fail(MPCX_EINVAL, "null argument");
+  if (B < 0) return fail(MPCX_EINVAL, "B < 0");
+  if (B == 0) return 0;
+  if (int r = check_bounds_vec(h, lbw, ubw)) return r;
+  HIPCHK(hipSetDevice(h->spec.device));
+  if (int r = ensure(h, B)) return r;
+  hipStream_t s = h->stream;
+  const double* dl = h->d_lbw;
+  const double* du = h->d_ubw;
+  if (lbw || ubw) {
+    std::vector<double> lb, ub;
+    spec_bounds(h->spec, lb, ub);
+    if (lbw) lb.assign(lbw, lbw + h->nw);
+    if (ubw) ub.assign(ubw, ubw + h->nw);
+    for (int i = 0; i < 3; ++i) {  // X_0 stays free: it is pinned by g_0
+      lb[i] = -1e20;
+      ub[i] = 1e20;
+    }
+    for (int i = 0; i < h->nw; ++i) {
+      if (!(lb[i] > -1e19)) lb[i] = -1e20;
+      if (!(ub[i] < 1e19)) ub[i] = 1e20;
+    }
+    HIPCHK(hipMemcpyAsync(h->d_lbw_call, lb.data(), h->nw * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->d_ubw_call, ub.data(), h->nw * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    dl = h->d_lbw_call;
+    du = h->d_ubw_call;
+  }
+  HIPCHK(hipMemcpyAsync(h->d_P, P, (size_t)B * h->np * sizeof(double), hipMemcpyHostToDevice, s));
+  if (w0) HIPCHK(hipMemcpyAsync(h->d_w0, w0, (size_t)B * h->nw * sizeof(double), hipMemcpyHostToDevice, s));
+  mpcx::SolveArgs a = make_args(h, B, h->d_P, w0 ? h->d_w0 : nullptr, dl, du, h->d_w, h->d_f,
+                                (lam_g ? h->d_lam : nullptr), h->d_status, h->d_iters);
+  HIPCHK(mpcx::launch_solve(a, s));
+  HIPCHK(hipMemcpyAsync(w_out, h->d_w, (size_t)B * h->nw * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (f_out) HIPCHK(hipMemcpyAsync(f_out, h->d_f, (size_t)B * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (lam_g) HIPCHK(hipMemcpyAsync(lam_g, h->d_lam, (size_t)B * h->ng * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (status) HIPCHK(hipMemcpyAsync(status, h->d_status, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (iters) HIPCHK(hipMemcpyAsync(iters, h->d_iters, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (g_out) {  // constraint values at the solution (host-side evaluation via the plant kernel)
+    const int N = h->spec.N;
+    std::vector<double> Pst((size_t)B * N * h->np), U((size_t)B * N * 2), XF((size_t)B * N * 3);
+    for (int b = 0; b < B; ++b) {
+      const double* w = w_out + (size_t)b * h->nw;
+      for (int k = 0; k < N; ++k) {
+        double* p = &Pst[((size_t)b * N + k) * h->np];
+        std::memcpy(p, P + (size_t)b * h->np, h->np * sizeof(double));
+        for (int i = 0; i < 3; ++i) p[i] = k == 0 ? w[i] : w[3 + 5 * (k - 1) + 2 + i];
+        if (h->spec.param_layout == MPCX_P_X0_STAGEREF)
+          for (int i = 0; i < 5; ++i) p[3 + i] = P[(size_t)b * h->np + 3 + 5 * k + i];
+        U[((size_t)b * N + k) * 2] = w[3 + 5 * k];
+        U[((size_t)b * N + k) * 2 + 1] = w[3 + 5 * k + 1];
+      }
+    }
+    if (int r = mpcx_plant_step(h, B * N, Pst.data(), U.data(), XF.data(), nullptr)) return r;
+    for (int b = 0; b < B; ++b) {
+      const double* w = w_out + (size_t)b * h->nw;
+      double* g = g_out + (size_t)b * h->ng;
+      for (int i = 0; i < 3; ++i) g[i] = P[(size_t)b * h->np + i] - w[i];
+      for (int k = 0; k < N; ++k)
+        for (int i = 0; i < 3; ++i) g[3 * (k + 1) + i] = XF[((size_t)b * N + k) * 3 + i] - w[3 + 5 * k + 2 + i];
+    }
+  }
+  return 0;
+}
+
+int mpcx_plant_step(mpcx_handle* h, int32_t B, const double* P, const double* u, double* xf, double* qf) {
+  if (!h || !P || !u || !xf) return fail(MPCX_EINVAL, "null argument");
+  if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
+  HIPCHK(hipSetDevice(h->spec.device));
+  hipStream_t s = h->stream;
+  double *dP = nullptr, *dU = nullptr, *dX = nullptr, *dQ = nullptr;
+  HIPCHK(hipMalloc(&dP, (size_t)B * h->np * sizeof(double)));
+  HIPCHK(hipMalloc(&dU, (size_t)B * 2 * sizeof(double)));
+  HIPCHK(hipMalloc(&dX, (size_t)B * 3 * sizeof(double)));
+  HIPCHK(hipMalloc(&dQ, (size_t)B * sizeof(double)));
+  HIPCHK(hipMemcpyAsync(dP, P, (size_t)B * h->np * sizeof(double), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(dU, u, (size_t)B * 2 * sizeof(double), hipMemcpyHostToDevice, s));
+  HIPCHK(mpcx::launch_plant(B, h->np, h->spec.param_layout, stage_params(h->spec), dP, dU, dX, dQ, s));
+  HIPCHK(hipMemcpyAsync(xf, dX, (size_t)B * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (qf) HIPCHK(hipMemcpyAsync(qf, dQ, (size_t)B * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  (void)hipFree(dP);
+  (void)hipFree(dU);
+  (void)hipFree(dX);
+  (void)hipFree(dQ);
+  return 0;
+}
+
+int mpcx_shift_dev(mpcx_handle* h, int32_t B, double* d_P, const double* d_w, double* d_w0_next, void* stream) {
+  if (!h || !d_P || !d_w || !d_w0_next) return fail(MPCX_EINVAL, "null argument");
+  if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
+  HIPCHK(hipSetDevice(h->spec.device));
+  HIPCHK(mpcx::launch_shift(B, h->spec.N, h->np, h->spec.param_layout, stage_params(h->spec), d_P, d_w, d_w0_next,
+                            (hipStream_t)stream));
+  return 0;
+}
+
+int mpcx_rk4_sens_dev(mpcx_handle* h, int32_t B, const double* d_X, const double* d_U, const double* d_xr,
+                      double* d_c, double* d_q, double* d_A, double* d_Bm, double* d_gq, void* stream) {
+  if (!h || !d_X || !d_U || !d_xr || !d_c || !d_q || !d_A || !d_Bm || !d_gq) return fail(MPCX_EINVAL, "null argument");
+  if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
+  if (h->spec.param_layout != MPCX_P_X0_XREF) return fail(MPCX_EINVAL, "rk4_sens_dev needs param_layout X0_XREF");
+  HIPCHK(hipSetDevice(h->spec.device));
+  HIPCHK(mpcx::launch_rk4_sens(B, h->spec.N, stage_params(h->spec), d_X, d_U, d_xr, d_c, d_q, d_A, d_Bm, d_gq,
+                               (hipStream_t)stream));
+  return 0;
+}
+
+int mpcx_rk4_sens(mpcx_handle* h, int32_t B, const double* w, const double* P, double* c, double* q, double* A,
+                  double* Bm, double* gq) {
+  if (!h || !w || !P || !c || !q || !A || !Bm || !gq) return fail(MPCX_EINVAL, "null argument");
+  if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
+  if (h->spec.param_layout != MPCX_P_X0_XREF) return fail(MPCX_EINVAL, "rk4_sens needs param_layout X0_XREF");
+  HIPCHK(hipSetDevice(h->spec.device));
+  const int N = h->spec.N;
+  const size_t nX = (size_t)(N + 1) * 3 * B, nU = (size_t)N * 2 * B, nR = (size_t)3 * B;
+  const size_t nC = (size_t)N * 3 * B, nQ = (size_t)N * B, nA = (size_t)N * 9 * B, nB = (size_t)N * 6 * B,
+               nG = (size_t)N * 5 * B;
+  const size_t total = nX + nU + nR + nC + nQ + nA + nB + nG;
+  if (total > h->cap_sweep) {
+    (void)hipFree(h->d_sweep);
+    h->d_sweep = nullptr;
+    h->cap_sweep = 0;
+    HIPCHK(hipMalloc(&h->d_sweep, total * sizeof(double)));
+    h->cap_sweep = total;
+  }
+  std::vector<double> hX(nX), hU(nU), hR(nR);
+  for (int b = 0; b < B; ++b) {
+    const double* wb = w + (size_t)b * h->nw;
+    for (int k = 0; k <= N; ++k)
+      for (int i = 0; i < 3; ++i) hX[((size_t)k * 3 + i) * B + b] = k == 0 ? wb[i] : wb[3 + 5 * (k - 1) + 2 + i];
+    for (int k = 0; k < N; ++k)
+      for (int i = 0; i < 2; ++i) hU[((size_t)k * 2 + i) * B + b] = wb[3 + 5 * k + i];
+    for (int i = 0; i < 3; ++i) hR[(size_t)i * B + b] = P[(size_t)b * h->np + 3 + i];
+  }
+  double* d = h->d_sweep;
+  double *dX = d, *dU = dX + nX, *dR = dU + nU, *dC = dR + nR, *dQ = dC + nC, *dA = dQ + nQ, *dB = dA + nA,
+         *dG = dB + nB;
+  hipStream_t s = h->stream;
+  HIPCHK(hipMemcpyAsync(dX, hX.data(), nX * sizeof(double), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(dU, hU.data(), nU * sizeof(double), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(dR, hR.data(), nR * sizeof(double), hipMemcpyHostToDevice, s));
+  HIPCHK(mpcx::launch_rk4_sens(B, N, stage_params(h->spec), dX, dU, dR, dC, dQ, dA, dB, dG, s));
+  std::vector<double> hC(nC), hQ(nQ), hA(nA), hB(nB), hG(nG);
+  HIPCHK(hipMemcpyAsync(hC.data(), dC, nC * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hQ.data(), dQ, nQ * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hA.data(), dA, nA * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hB.data(), dB, nB * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hG.data(), dG, nG * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (int b = 0; b < B; ++b)
+    for (int k = 0; k < N; ++k) {
+      const size_t o = (size_t)b * N + k;
+      for (int i = 0; i < 3; ++i) c[o * 3 + i] = hC[((size_t)k * 3 + i) * B + b];
+      q[o] = hQ[(size_t)k * B + b];
+      for (int i = 0; i < 9; ++i) A[o * 9 + i] = hA[((size_t)k * 9 + i) * B + b];
+      for (int i = 0; i < 6; ++i) Bm[o * 6 + i] = hB[((size_t)k * 6 + i) * B + b];
+      for (int i = 0; i < 5; ++i) gq[o * 5 + i] = hG[((size_t)k * 5 + i) * B + b];
+    }
+  return 0;
+}
+
+}  // extern "C"

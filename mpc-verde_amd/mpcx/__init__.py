@@ -1,0 +1,8 @@
+"""mpcx -- MI355X-native batched multiple-shooting MPC (drop-in for the CasADi/IPOPT
+hot path of gabrielhaj/mpc-verde).  See DESIGN.md and include/mpcx.h."""
+from .ocp import OCP, unicycle_point_to_point, unicycle_tracking, to_spec  # noqa: F401
+from .nlpsol import Solver, Integrator, nlpsol, integrator  # noqa: F401
+from . import _lib  # noqa: F401
+
+__all__ = ["OCP", "unicycle_point_to_point", "unicycle_tracking", "to_spec", "Solver", "Integrator", "nlpsol",
+           "integrator"]

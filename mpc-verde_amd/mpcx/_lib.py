@@ -1,0 +1,128 @@
+"""ctypes binding of ``libmpcx.so`` (the C ABI declared in ``include/mpcx.h``).
+
+The HIP library is the only compute path: if it is missing or cannot be loaded
+this module raises immediately -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmpcx.so")
+
+MODEL_UNICYCLE = 1
+COST_QUADRATURE = 0
+COST_NODE = 1
+P_X0_XREF = 0
+P_X0_STAGEREF = 1
+
+STATUS = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Maximum_Iterations_Exceeded",
+          3: "Solve_Failed"}
+
+# C-ABI entry points (include/mpcx.h) -- checked by tests/test_capi_symbols.py
+EXPORTS = ("mpcx_default_spec", "mpcx_create", "mpcx_destroy", "mpcx_last_error", "mpcx_dims", "mpcx_solve_batch",
+           "mpcx_solve_batch_dev", "mpcx_plant_step", "mpcx_shift_dev", "mpcx_rk4_sens", "mpcx_rk4_sens_dev")
+
+
+class Spec(ctypes.Structure):
+    """Mirror of ``mpcx_spec`` (include/mpcx.h)."""
+
+    _fields_ = [("model", ctypes.c_int32), ("cost", ctypes.c_int32), ("param_layout", ctypes.c_int32),
+                ("N", ctypes.c_int32), ("M", ctypes.c_int32), ("max_iter", ctypes.c_int32),
+                ("device", ctypes.c_int32), ("reserved", ctypes.c_int32), ("T", ctypes.c_double),
+                ("tol", ctypes.c_double), ("Q", ctypes.c_double * 8), ("R", ctypes.c_double * 8),
+                ("lbu", ctypes.c_double * 8), ("ubu", ctypes.c_double * 8), ("lbx", ctypes.c_double * 8),
+                ("ubx", ctypes.c_double * 8)]
+
+
+_lib = None
+
+
+class MpcxError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libmpcx.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MpcxError(f"{LIB_PATH} not found: build it with `make -C mpc-verde_amd` (hipcc, gfx950)")
+    lib = ctypes.CDLL(LIB_PATH)
+    dp = ctypes.POINTER(ctypes.c_double)
+    ip = ctypes.POINTER(ctypes.c_int32)
+    vp = ctypes.c_void_p
+    H = ctypes.c_void_p
+    lib.mpcx_default_spec.argtypes = [ctypes.POINTER(Spec), ctypes.c_int32, ctypes.c_int32]
+    lib.mpcx_create.argtypes = [ctypes.POINTER(Spec), ctypes.POINTER(H)]
+    lib.mpcx_destroy.argtypes = [H]
+    lib.mpcx_destroy.restype = None
+    lib.mpcx_last_error.restype = ctypes.c_char_p
+    lib.mpcx_dims.argtypes = [H, ip, ip, ip]
+    lib.mpcx_solve_batch.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp, dp, dp, dp, dp, ip, ip]
+    lib.mpcx_solve_batch_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.mpcx_plant_step.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp]
+    lib.mpcx_shift_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp]
+    lib.mpcx_rk4_sens.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp, dp, dp, dp]
+    lib.mpcx_rk4_sens_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    for name in EXPORTS:
+        getattr(lib, name)  # AttributeError if an export is missing
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = load().mpcx_last_error().decode(errors="replace")
+        raise MpcxError(f"mpcx error {rc}: {msg}")
+
+
+def dptr(a):
+    """double* of a C-contiguous float64 ndarray (or None)."""
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def iptr(a):
+    if a is None:
+        return None
+    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+class Handle:
+    """Owning wrapper of an ``mpcx_handle*``."""
+
+    def __init__(self, spec: Spec):
+        lib = load()
+        self._spec = spec
+        self._h = ctypes.c_void_p()
+        check(lib.mpcx_create(ctypes.byref(spec), ctypes.byref(self._h)))
+        nw, ng, npar = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        check(lib.mpcx_dims(self._h, ctypes.byref(nw), ctypes.byref(ng), ctypes.byref(npar)))
+        self.n_w, self.n_g, self.n_p = nw.value, ng.value, npar.value
+
+    @property
+    def ptr(self):
+        return self._h
+
+    @property
+    def spec(self):
+        return self._spec
+
+    def close(self):
+        if self._h:
+            load().mpcx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

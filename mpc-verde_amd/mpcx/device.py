@@ -1,0 +1,66 @@
+"""Device-resident batched receding-horizon loop (torch tensors as device memory).
+
+PyTorch provides device allocations, streams and events only; all arithmetic is
+in libmpcx's HIP kernels, reached through the ``*_dev`` C entry points.  One
+closed-loop step for B instances = one fused solve launch + one shift/plant
+launch (``Casadi/multiple_shooting_casadi.py:226-287``, batched), with no host
+synchronisation in between.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .nlpsol import Solver
+
+
+def _ptr(t):
+    return None if t is None else ctypes_void(t.data_ptr())
+
+
+def ctypes_void(p):
+    import ctypes
+
+    return ctypes.c_void_p(p)
+
+
+class DeviceLoop:
+    """B independent MPC instances stepped on one GPU.
+
+    P (B, n_p) float64 parameters live on the device; w holds the last solution
+    and w0 the shifted warm start.  ``step()`` enqueues a solve and the plant
+    update on ``stream`` and returns immediately.
+    """
+
+    def __init__(self, solver: Solver, P0, device="cuda", stream=None, cold_first=True):
+        self.solver = solver
+        self.device = torch.device(device)
+        P0 = np.ascontiguousarray(np.asarray(P0, np.float64))
+        self.B = P0.shape[0]
+        nw, ng = solver._h.n_w, solver._h.n_g
+        self.P = torch.from_numpy(P0).to(self.device)
+        self.w = torch.zeros((self.B, nw), dtype=torch.float64, device=self.device)
+        self.w0 = torch.zeros((self.B, nw), dtype=torch.float64, device=self.device)
+        self.f = torch.zeros(self.B, dtype=torch.float64, device=self.device)
+        self.status = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        self.iters = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self._cold = cold_first
+
+    def solve(self):
+        lib = _lib.load()
+        s = ctypes_void(self.stream.cuda_stream)
+        w0 = None if self._cold else _ptr(self.w0)
+        _lib.check(lib.mpcx_solve_batch_dev(self.solver._h.ptr, self.B, _ptr(self.P), w0, _ptr(self.w),
+                                            _ptr(self.f), None, _ptr(self.status), _ptr(self.iters), s))
+        self._cold = False
+
+    def shift(self):
+        lib = _lib.load()
+        s = ctypes_void(self.stream.cuda_stream)
+        _lib.check(lib.mpcx_shift_dev(self.solver._h.ptr, self.B, _ptr(self.P), _ptr(self.w), _ptr(self.w0), s))
+
+    def step(self):
+        self.solve()
+        self.shift()

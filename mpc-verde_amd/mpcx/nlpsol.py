@@ -1,0 +1,246 @@
+"""CasADi-``nlpsol``-shaped façade over libmpcx (the drop-in for the hot path).
+
+Reference boundary (``Casadi/multiple_shooting_casadi.py``):
+
+    solver = ca.nlpsol('solver', 'ipopt', prob, opts)                       # :197
+    sol = solver(x0=w0, lbx=lbw, ubx=ubw, lbg=lbg, ubg=ubg, p=P)           # :235-242
+    u = sol['x'][3:5] ...                                                   # :243-256
+    state_init = F(args['p'], u[:, 0])[0]                                   # :273
+
+Here:
+
+    solver = mpcx.nlpsol('solver', 'mi355x', ocp, opts)
+    sol = solver(x0=w0, lbx=lbw, ubx=ubw, lbg=lbg, ubg=ubg, p=P)
+    F = mpcx.integrator(ocp)
+
+``sol`` holds numpy column vectors with CasADi's shapes and sign conventions:
+'x' (n_w,1), 'f' (1,1), 'g' (n_g,1), 'lam_g' (n_g,1), 'lam_x' (n_w,1),
+'lam_p' (n_p,1; zeros).  ``solver.stats()`` mirrors CasADi's stats dict
+('return_status', 'success', 'iter_count', 't_wall_total').  Batched use:
+``solver.solve_batch(P, w0)``.  Every call runs the HIP kernel on the GPU.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+
+from . import _lib
+from .ocp import OCP, to_spec
+
+
+def _vec(v, n, name, fill=None):
+    """CasADi-style input coercion: list / ndarray / DM-like / scalar (broadcast)."""
+    if v is None:
+        if fill is None:
+            return None
+        return np.full(n, float(fill))
+    a = np.asarray(v, dtype=np.float64).reshape(-1)
+    if a.size == 1 and n != 1:
+        a = np.full(n, float(a[0]))
+    if a.size != n:
+        raise ValueError(f"{name}: expected {n} entries, got {a.size}")
+    return np.ascontiguousarray(a)
+
+
+class Solver:
+    """Callable returned by :func:`nlpsol`."""
+
+    def __init__(self, name: str, ocp: OCP, opts: dict | None = None, device: int = 0):
+        opts = dict(opts or {})
+        ip = dict(opts.get("ipopt", {}))
+        self.name = name
+        self.ocp = ocp
+        self.max_iter = int(ip.pop("max_iter", 3000))
+        self.tol = float(ip.pop("tol", 1e-8))
+        # accepted for source compatibility with :188-196; they do not change the optimum
+        for k in ("print_level", "acceptable_tol", "acceptable_obj_change_tol", "acceptable_iter", "sb"):
+            ip.pop(k, None)
+        if ip:
+            raise ValueError(f"unsupported ipopt options: {sorted(ip)}")
+        self._h = _lib.Handle(to_spec(ocp, self.max_iter, self.tol, device))
+        self._stats = {}
+
+    # ---------------------------------------------------------------- layout
+    @property
+    def n_w(self):
+        return self.ocp.N * 2 if self.ocp.formulation == "single_shooting" else self._h.n_w
+
+    @property
+    def n_g(self):
+        return self.ocp.N * 2 if self.ocp.formulation == "single_shooting" else self._h.n_g
+
+    @property
+    def n_p(self):
+        return self._h.n_p
+
+    def stats(self):
+        return dict(self._stats)
+
+    # ---------------------------------------------------------------- batched core
+    def solve_batch(self, P, w0=None, lbw=None, ubw=None, want_lam=True, want_g=False):
+        """Solve B independent NLPs (multiple-shooting layout).
+
+        P (B, n_p); w0 (B, n_w) or None (cold start X_k = x0, U = 0).
+        Returns dict of arrays: w (B,n_w), f (B,), lam_g (B,n_g), status (B,), iters (B,), g (B,n_g).
+        """
+        P = np.ascontiguousarray(np.atleast_2d(np.asarray(P, np.float64)))
+        B = P.shape[0]
+        if P.shape[1] != self._h.n_p:
+            raise ValueError(f"P: expected {self._h.n_p} columns, got {P.shape[1]}")
+        nw, ng = self._h.n_w, self._h.n_g
+        w0a = None
+        if w0 is not None:
+            w0a = np.ascontiguousarray(np.asarray(w0, np.float64).reshape(B, nw))
+        w = np.empty((B, nw))
+        f = np.empty(B)
+        lam = np.empty((B, ng)) if want_lam else None
+        g = np.empty((B, ng)) if want_g else None
+        st = np.empty(B, np.int32)
+        it = np.empty(B, np.int32)
+        lib = _lib.load()
+        t0 = time.perf_counter()
+        _lib.check(lib.mpcx_solve_batch(self._h.ptr, B, _lib.dptr(P), _lib.dptr(w0a), _lib.dptr(lbw), _lib.dptr(ubw),
+                                        _lib.dptr(w), _lib.dptr(f), _lib.dptr(g), _lib.dptr(lam), _lib.iptr(st),
+                                        _lib.iptr(it)))
+        t = time.perf_counter() - t0
+        return {"w": w, "f": f, "lam_g": lam, "g": g, "status": st, "iters": it, "t_wall": t}
+
+    def rk4_sens(self, w, P):
+        """Per-interval defects, costs and Jacobians at w (B, n_w) -- the sweep kernel."""
+        w = np.ascontiguousarray(np.atleast_2d(np.asarray(w, np.float64)))
+        P = np.ascontiguousarray(np.atleast_2d(np.asarray(P, np.float64)))
+        B, N = w.shape[0], self.ocp.N
+        c = np.empty((B, N, 3))
+        q = np.empty((B, N))
+        A = np.empty((B, N, 3, 3))
+        Bm = np.empty((B, N, 3, 2))
+        gq = np.empty((B, N, 5))
+        _lib.check(_lib.load().mpcx_rk4_sens(self._h.ptr, B, _lib.dptr(w), _lib.dptr(P), _lib.dptr(c), _lib.dptr(q),
+                                             _lib.dptr(A), _lib.dptr(Bm), _lib.dptr(gq)))
+        return {"c": c, "q": q, "A": A, "B": Bm, "gq": gq}
+
+    def lam_x(self, w, P, lam_g):
+        """Bound multipliers in CasADi's convention: grad f + J^T lam_g + lam_x = 0."""
+        s = self.rk4_sens(w, P)
+        B, N = s["q"].shape
+        r = np.zeros((B, self._h.n_w))
+        lam_g = np.asarray(lam_g).reshape(B, -1)
+        ix = lambda k: np.arange(3) if k == 0 else 3 + 5 * (k - 1) + 2 + np.arange(3)  # noqa: E731
+        r[:, 0:3] -= lam_g[:, 0:3]
+        for k in range(N):
+            l1 = lam_g[:, 3 * (k + 1):3 * (k + 2)]
+            r[:, ix(k)] += s["gq"][:, k, 0:3] + np.einsum("bij,bi->bj", s["A"][:, k], l1)
+            r[:, 3 + 5 * k:5 + 5 * k] += s["gq"][:, k, 3:5] + np.einsum("bij,bi->bj", s["B"][:, k], l1)
+            r[:, ix(k + 1)] -= l1
+        return -r
+
+    # ---------------------------------------------------------------- CasADi-shaped call
+    def __call__(self, x0=None, lbx=None, ubx=None, lbg=None, ubg=None, p=None, lam_x0=None, lam_g0=None):
+        if p is None:
+            raise ValueError("p is required")
+        ocp = self.ocp
+        P = _vec(p, self._h.n_p, "p")[None, :]
+        ss = ocp.formulation == "single_shooting"
+        lbx = _vec(lbx, self.n_w, "lbx", -math.inf)
+        ubx = _vec(ubx, self.n_w, "ubx", math.inf)
+        lbg = _vec(lbg, self.n_g, "lbg", 0.0 if not ss else -math.inf)
+        ubg = _vec(ubg, self.n_g, "ubg", 0.0 if not ss else math.inf)
+        if ss:
+            if np.any(np.isfinite(lbg)) or np.any(np.isfinite(ubg)):
+                raise ValueError("single shooting: only inactive (+-inf) bounds on g are supported")
+        elif np.any(lbg != 0) or np.any(ubg != 0):
+            raise ValueError("multiple shooting: g are the shooting equalities, lbg = ubg = 0 required")
+        N = ocp.N
+        if ss:  # decision = U; bounds on U map onto the U slots of the multiple-shooting w
+            lbw = np.full(self._h.n_w, -1e20)
+            ubw = np.full(self._h.n_w, 1e20)
+            for k in range(N):
+                lbw[3 + 5 * k:5 + 5 * k] = lbx[2 * k:2 * k + 2]
+                ubw[3 + 5 * k:5 + 5 * k] = ubx[2 * k:2 * k + 2]
+            w0 = None
+            if x0 is not None:
+                U = _vec(x0, 2 * N, "x0").reshape(N, 2)
+                X = self._rollout(P[0], U)
+                w0 = np.concatenate([X[0]] + [np.concatenate([U[k], X[k + 1]]) for k in range(N)])[None, :]
+        else:
+            lbw, ubw = lbx, ubx
+            w0 = None if x0 is None else _vec(x0, self._h.n_w, "x0")[None, :]
+        lbw = np.where(np.isfinite(lbw), lbw, -1e20)
+        ubw = np.where(np.isfinite(ubw), ubw, 1e20)
+        r = self.solve_batch(P, w0, np.ascontiguousarray(lbw), np.ascontiguousarray(ubw), want_lam=True,
+                             want_g=True)
+        st = int(r["status"][0])
+        self._stats = {"return_status": _lib.STATUS.get(st, str(st)), "success": st <= 1,
+                       "iter_count": int(r["iters"][0]), "t_wall_total": r["t_wall"], "status_code": st}
+        w = r["w"][0]
+        lam_x = self.lam_x(r["w"], P, r["lam_g"])[0]
+        if ss:
+            U = np.stack([w[3 + 5 * k:5 + 5 * k] for k in range(N)]).reshape(-1)
+            Xs = np.stack([w[5 + 5 * k:8 + 5 * k] for k in range(N)])
+            g = Xs[:, 0:2].reshape(-1)
+            lx = np.concatenate([lam_x[3 + 5 * k:5 + 5 * k] for k in range(N)])
+            return {"x": U[:, None], "f": np.array([[r["f"][0]]]), "g": g[:, None],
+                    "lam_g": np.zeros((2 * N, 1)), "lam_x": lx[:, None], "lam_p": np.zeros((self._h.n_p, 1))}
+        return {"x": w[:, None], "f": np.array([[r["f"][0]]]), "g": r["g"][0][:, None],
+                "lam_g": r["lam_g"][0][:, None], "lam_x": lam_x[:, None], "lam_p": np.zeros((self._h.n_p, 1))}
+
+    def _rollout(self, P, U):
+        N = self.ocp.N
+        X = [np.asarray(P[0:3], float)]
+        F = Integrator(self.ocp, handle=self._h)
+        for k in range(N):
+            p = np.array(P, float).copy()
+            p[0:3] = X[-1]
+            if self.ocp.param == "x0_stageref":
+                p[3:8] = P[3 + 5 * k:8 + 5 * k]
+            X.append(F(p, U[k])[0].reshape(-1))
+        return np.array(X)
+
+
+class Integrator:
+    """``F = ca.Function('F', [P, U], [X, Q], ['x0','p'], ['xf','qf'])`` (:114).
+
+    ``F(p, u)`` -> [xf (3,1), qf (1,1)];  ``F(x0=p, p=u)`` -> {'xf', 'qf'};
+    ``F.batch(P, U)`` -> (xf (B,3), qf (B,)).  Evaluated by the plant kernel.
+    """
+
+    def __init__(self, ocp: OCP, device: int = 0, handle=None):
+        self.ocp = ocp
+        self._h = handle if handle is not None else _lib.Handle(to_spec(ocp, device=device))
+
+    def batch(self, P, U):
+        P = np.ascontiguousarray(np.atleast_2d(np.asarray(P, np.float64)))
+        U = np.ascontiguousarray(np.atleast_2d(np.asarray(U, np.float64)))
+        B = P.shape[0]
+        if U.shape != (B, 2):
+            raise ValueError("U must be (B, 2)")
+        xf = np.empty((B, 3))
+        qf = np.empty(B)
+        _lib.check(_lib.load().mpcx_plant_step(self._h.ptr, B, _lib.dptr(P), _lib.dptr(U), _lib.dptr(xf),
+                                               _lib.dptr(qf)))
+        return xf, qf
+
+    def __call__(self, *args, **kw):
+        if kw:
+            p = kw.get("x0")
+            u = kw.get("p")
+            xf, qf = self.batch(_vec(p, self._h.n_p, "x0")[None, :], _vec(u, 2, "p")[None, :])
+            return {"xf": xf[0][:, None], "qf": qf[:, None]}
+        p, u = args
+        xf, qf = self.batch(_vec(p, self._h.n_p, "p")[None, :], _vec(u, 2, "u")[None, :])
+        return [xf[0][:, None], qf[:, None]]
+
+
+def nlpsol(name: str, plugin: str, prob: OCP, opts: dict | None = None, device: int = 0) -> Solver:
+    """Create a solver (``ca.nlpsol`` signature).  plugin must be 'mi355x'."""
+    if plugin not in ("mi355x",):
+        raise ValueError(f"unknown plugin {plugin!r} (available: 'mi355x')")
+    if not isinstance(prob, OCP):
+        raise TypeError("prob must be an mpcx.OCP (symbolic CasADi problems are not supported)")
+    return Solver(name, prob, opts, device)
+
+
+def integrator(ocp: OCP, device: int = 0) -> Integrator:
+    return Integrator(ocp, device)

@@ -1,0 +1,101 @@
+"""Problem descriptions: the NLPs the reference scripts build symbolically.
+
+CasADi receives ``prob = {'f': J, 'x': w, 'g': g, 'p': P}`` as symbolic
+expressions.  CasADi is not the product here, so a problem is described by the
+few numbers that determine those expressions; :func:`to_spec` turns one into
+the C ``mpcx_spec``.  Each builder cites the script whose NLP it reproduces.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+from . import _lib
+
+
+@dataclasses.dataclass
+class OCP:
+    """Multiple-shooting OCP of ``Casadi/multiple_shooting_casadi.py:30-178``.
+
+    formulation = "multiple_shooting": decision vector w = [X_0 | U_0 X_1 | ...]
+                  (interleaved, :128-170), g = [P[:3]-X_0; F(X_k,U_k).xf - X_{k+1}].
+    formulation = "single_shooting": decision vector = U (interleaved v, w),
+                  g = (x_k, y_k) k=1..N with +-inf bounds
+                  (``Casadi/single_shooting_v2.py:115-158``).
+    cost = "quadrature" (RK4-integrated L, CasADi scripts) or "node" (mpctools).
+    param = "x0_xref": p = [x0; x_ref] (6); "x0_stageref": p = [x0; (x_ref_k, u_ref_k)_k].
+    """
+
+    N: int = 10
+    T: float = 0.2
+    M: int = 4
+    Q: tuple = (1.0, 5.0, 0.1)
+    R: tuple = (0.5, 0.05)
+    u_lb: tuple = (-1.0, -math.pi / 4)
+    u_ub: tuple = (1.0, math.pi / 4)
+    x_lb: tuple = (-math.inf, -math.inf, -math.inf)
+    x_ub: tuple = (math.inf, math.inf, math.inf)
+    cost: str = "quadrature"
+    param: str = "x0_xref"
+    formulation: str = "multiple_shooting"
+    model: str = "unicycle"
+
+    @property
+    def nx(self):
+        return 3
+
+    @property
+    def nu(self):
+        return 2
+
+    @property
+    def n_w_ms(self):
+        return 3 + 5 * self.N
+
+    @property
+    def n_g_ms(self):
+        return 3 * (self.N + 1)
+
+    @property
+    def n_p(self):
+        return 6 if self.param == "x0_xref" else 3 + 5 * self.N
+
+
+def unicycle_point_to_point(N=10, T=0.2, M=4, v_max=1.0, omega_max=math.pi / 4, Q=(1.0, 5.0, 0.1), R=(0.5, 0.05),
+                            formulation="multiple_shooting"):
+    """``Casadi/multiple_shooting_casadi.py:30-114`` (and ``single_shooting_v2.py``)."""
+    return OCP(N=N, T=T, M=M, Q=tuple(Q), R=tuple(R), u_lb=(-v_max, -omega_max), u_ub=(v_max, omega_max),
+               formulation=formulation)
+
+
+def unicycle_tracking(N=10, T=0.2):
+    """``Trajectory Tracking/Trajectory_tracking.py:15-72``: RK4 with M=1, node cost
+    l(x,u,p_k) with Q=diag(1,1,0.1), R=diag(0.5,0.05), per-stage reference
+    p_k = (x_r, y_r, th_r, v_r, w_r), bounds |v|<=1, |w|<=pi/4, x in [-20,20], y in [-2,2]."""
+    return OCP(N=N, T=T, M=1, Q=(1.0, 1.0, 0.1), R=(0.5, 0.05), x_lb=(-20.0, -2.0, -math.inf),
+               x_ub=(20.0, 2.0, math.inf), cost="node", param="x0_stageref")
+
+
+def to_spec(ocp: OCP, max_iter=2000, tol=1e-8, device=0) -> _lib.Spec:
+    if ocp.model != "unicycle":
+        raise ValueError(f"unsupported model {ocp.model!r}")
+    s = _lib.Spec()
+    s.model = _lib.MODEL_UNICYCLE
+    s.cost = {"quadrature": _lib.COST_QUADRATURE, "node": _lib.COST_NODE}[ocp.cost]
+    s.param_layout = {"x0_xref": _lib.P_X0_XREF, "x0_stageref": _lib.P_X0_STAGEREF}[ocp.param]
+    s.N, s.M, s.max_iter, s.device = int(ocp.N), int(ocp.M), int(max_iter), int(device)
+    s.T, s.tol = float(ocp.T), float(tol)
+    big = 1e20
+
+    def fin(v, default):
+        return default if not math.isfinite(v) else float(v)
+
+    for i in range(3):
+        s.Q[i] = float(ocp.Q[i])
+        s.lbx[i] = fin(ocp.x_lb[i], -big)
+        s.ubx[i] = fin(ocp.x_ub[i], big)
+    for i in range(2):
+        s.R[i] = float(ocp.R[i])
+        s.lbu[i] = float(ocp.u_lb[i])
+        s.ubu[i] = float(ocp.u_ub[i])
+    return s

@@ -1,0 +1,113 @@
+"""ctypes loader for the C++ CPU oracle ``oracle/libipm_ref.so``.
+
+TEST INFRASTRUCTURE ONLY (tests/, __graft_entry__.smoke(), bench.py cpu_baseline).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class OracleSpec(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_int32), ("M", ctypes.c_int32), ("cost", ctypes.c_int32),
+                ("max_iter", ctypes.c_int32), ("T", ctypes.c_double), ("Q", ctypes.c_double * 3),
+                ("R", ctypes.c_double * 2), ("tol", ctypes.c_double)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "libipm_ref.so")
+        if not os.path.exists(path):
+            build()
+        _LIB = ctypes.CDLL(path)
+        dp = ctypes.POINTER(ctypes.c_double)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        _LIB.oracle_solve_batch.argtypes = [ctypes.POINTER(OracleSpec), ctypes.c_int, dp, ctypes.c_int, dp, dp, dp,
+                                            dp, dp, dp, dp, ip, ip, ctypes.c_int]
+        _LIB.oracle_stage.argtypes = [ctypes.POINTER(OracleSpec), ctypes.c_int, dp, dp, dp, dp, dp, dp, dp, dp, dp]
+    return _LIB
+
+
+def _p(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _spec(ocp, max_iter=200, tol=1e-8):
+    s = OracleSpec()
+    s.N, s.M = ocp.N, ocp.M
+    s.cost = 0 if ocp.cost == "quadrature" else 1
+    s.max_iter = max_iter
+    s.T = ocp.T
+    s.Q[:] = list(ocp.Q)
+    s.R[:] = list(ocp.R)
+    s.tol = tol
+    return s
+
+
+def solve_batch(ocp, P, w0=None, pstage=None, lbw=None, ubw=None, max_iter=200, tol=1e-8, nthreads=0):
+    """Batched IPM solve on the CPU.  Returns dict(w, lam_g, f, status, iters)."""
+    from . import nlp_ref
+    P = np.ascontiguousarray(P, dtype=np.float64)
+    B = P.shape[0]
+    nw, ng = nlp_ref.n_w(ocp.N), nlp_ref.n_g(ocp.N)
+    lb, ub = nlp_ref.ms_bounds(ocp)
+    lb = np.ascontiguousarray(lb if lbw is None else lbw, dtype=np.float64)
+    ub = np.ascontiguousarray(ub if ubw is None else ubw, dtype=np.float64)
+    lb = np.where(np.isfinite(lb), lb, -1e20)
+    ub = np.where(np.isfinite(ub), ub, 1e20)
+    w0a = None if w0 is None else np.ascontiguousarray(w0, dtype=np.float64).reshape(B, nw)
+    ps = None if pstage is None else np.ascontiguousarray(pstage, dtype=np.float64).reshape(B, ocp.N, 5)
+    w = np.zeros((B, nw))
+    lam = np.zeros((B, ng))
+    f = np.zeros(B)
+    st = np.zeros(B, np.int32)
+    it = np.zeros(B, np.int32)
+    spec = _spec(ocp, max_iter, tol)
+    lib().oracle_solve_batch(ctypes.byref(spec), B, _p(P), P.shape[1], _p(ps), _p(w0a), _p(lb), _p(ub), _p(w),
+                             _p(lam), _p(f), st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                             it.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), nthreads)
+    return {"w": w, "lam_g": lam, "f": f, "status": st, "iters": it}
+
+
+def stage(ocp, x, u, xr, ur=None, lam=None):
+    """Interval map + Jacobian (B,4,5) + packed Hessian of qf + lam^T xf (B,15)."""
+    x = np.ascontiguousarray(x, np.float64).reshape(-1, 3)
+    B = x.shape[0]
+    u = np.ascontiguousarray(u, np.float64).reshape(B, 2)
+    xr = np.ascontiguousarray(np.broadcast_to(xr, (B, 3)), np.float64)
+    ur = None if ur is None else np.ascontiguousarray(np.broadcast_to(ur, (B, 2)), np.float64)
+    lam = None if lam is None else np.ascontiguousarray(np.broadcast_to(lam, (B, 3)), np.float64)
+    xf = np.zeros((B, 3))
+    qf = np.zeros(B)
+    jac = np.zeros((B, 4, 5))
+    hess = np.zeros((B, 15))
+    spec = _spec(ocp)
+    lib().oracle_stage(ctypes.byref(spec), B, _p(x), _p(u), _p(xr), _p(ur), _p(lam), _p(xf), _p(qf), _p(jac),
+                       _p(hess))
+    return xf, qf, jac, hess
+
+
+def unpack_sym5(h):
+    """packed upper-triangular (…,15) -> (…,5,5)."""
+    h = np.asarray(h)
+    H = np.zeros(h.shape[:-1] + (5, 5))
+    t = 0
+    for i in range(5):
+        for j in range(i, 5):
+            H[..., i, j] = h[..., t]
+            H[..., j, i] = h[..., t]
+            t += 1
+    return H

@@ -1,0 +1,272 @@
+"""GPU parity tests: the HIP path (through the C ABI / ctypes façade) vs the oracles.
+
+Oracles: oracle/nlp_ref.py (NumPy, projected Newton, complex-step derivatives)
+and oracle/libipm_ref.so (C++ IPOPT-style IPM, jet derivatives); both pinned
+to the reference's CasADi+IPOPT outputs (tests/golden).  Tolerances follow
+SURVEY.md §4 / BASELINE.json: solution error <= 1e-4 relative to
+max(||u||_inf, 1e-3) against IPOPT; kernel-level outputs <= 1e-12 relative.
+"""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-4  # north_star: optimal (x*, u*) within 1e-4 relative of CasADi/IPOPT
+
+
+def rel_err(a, b):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-3))
+
+
+@pytest.fixture(scope="module")
+def mpcx():
+    import mpcx as m
+
+    m._lib.load()
+    return m
+
+
+@pytest.fixture(scope="module")
+def R():
+    from oracle import nlp_ref
+
+    return nlp_ref
+
+
+@pytest.fixture(scope="module")
+def C():
+    from oracle import ipm_ref
+
+    ipm_ref.lib()
+    return ipm_ref
+
+
+def config2_batch(B=1024, seed=20261015, golden_rows=None):
+    """SURVEY.md §8(d) config 2 inputs: instances 0..83 = golden P_j, rest random."""
+    from oracle import nlp_ref
+
+    rng = np.random.default_rng(seed)
+    P = np.zeros((B, 6))
+    P[:, 3:6] = (10.0, 10.0, 0.0)
+    n0 = 0
+    if golden_rows is not None:
+        Pg, _ = nlp_ref.golden_pairs(golden_rows)
+        n0 = min(B, Pg.shape[0])
+        P[:n0] = Pg[:n0]
+    P[n0:, 0:2] = rng.uniform(-5, 5, size=(B - n0, 2))
+    P[n0:, 2] = rng.uniform(-np.pi / 2, np.pi / 2, size=B - n0)
+    return P
+
+
+# ----------------------------------------------------------------------------- kernel level
+def test_rk4_sens_matches_oracle(mpcx, R):
+    """Sweep kernel outputs (defect, q, A, B, grad q) vs complex-step oracle, <= 1e-12."""
+    ocp = mpcx.unicycle_point_to_point(N=20)
+    solver = mpcx.nlpsol("s", "mi355x", ocp)
+    rng = np.random.default_rng(1)
+    B = 37
+    P = np.zeros((B, 6))
+    P[:, 0:3] = rng.normal(size=(B, 3)) * 3
+    P[:, 3:6] = rng.normal(size=(B, 3)) * 5
+    w = rng.normal(size=(B, solver.n_w))
+    w[:, 3::5] = rng.uniform(-1, 1, size=(B, 20))
+    out = solver.rk4_sens(w, P)
+    rocp = R.UnicycleOCP(N=20)
+    X, U = R.split_w(w, 20)
+    xr = np.broadcast_to(P[:, None, 3:6], (B, 20, 3))
+    xf, qf = R.F(X[:, :-1], U, xr, rocp)
+    jac = R.stage_jacobian(X[:, :-1], U, xr, rocp)
+    scale = lambda a: max(1.0, float(np.max(np.abs(a))))  # noqa: E731
+    assert np.max(np.abs(out["c"] - (xf - X[:, 1:]))) <= 1e-12 * scale(xf)
+    assert np.max(np.abs(out["q"] - qf)) <= 1e-12 * scale(qf)
+    assert np.max(np.abs(out["A"] - jac[..., 0:3, 0:3])) <= 1e-12 * scale(jac)
+    assert np.max(np.abs(out["B"] - jac[..., 0:3, 3:5])) <= 1e-12 * scale(jac)
+    assert np.max(np.abs(out["gq"] - jac[..., 3, :])) <= 1e-12 * scale(jac[..., 3, :])
+
+
+def test_plant_replays_golden_closed_loop(mpcx, R, golden):
+    """F (plant kernel) reproduces the 83 recorded state transitions of 1exemplo.xlsx."""
+    rows = np.array(golden["multiple_shooting"]["rows"])
+    F = mpcx.integrator(mpcx.unicycle_point_to_point(N=10))
+    P = np.zeros((rows.shape[0] - 2, 6))
+    P[:, 0:3] = rows[1:-1, 0:3]
+    P[:, 3:6] = (10, 10, 0)
+    xf, _ = F.batch(P, rows[:-2, 3:5])
+    assert np.max(np.abs(xf - rows[2:, 0:3])) < 1e-12
+    # CasADi call shapes
+    out = F(P[0], rows[0, 3:5])
+    assert out[0].shape == (3, 1) and out[1].shape == (1, 1)
+    d = F(x0=P[0], p=rows[0, 3:5])
+    assert set(d) == {"xf", "qf"}
+
+
+# ----------------------------------------------------------------------------- golden (IPOPT) pins
+def test_golden_pairs_cold_start(mpcx, R, golden):
+    """All 84 recorded IPOPT solves (P_j -> u0*_j, N=10) in ONE batch, cold start."""
+    rows = np.array(golden["multiple_shooting"]["rows"])
+    P, U0 = R.golden_pairs(rows)
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=10))
+    r = solver.solve_batch(P)
+    assert np.all(r["status"] == 0), np.bincount(r["status"])
+    u0 = r["w"][:, 3:5]
+    errs = [rel_err(u0[j], U0[j]) for j in range(len(U0))]
+    assert max(errs) <= REL_TOL, max(errs)
+
+
+def test_casadi_call_shapes_and_closed_loop(mpcx, R, golden):
+    """The reference's driver loop (Casadi/multiple_shooting_casadi.py:224-298), with
+    ca.nlpsol swapped for mpcx.nlpsol, reproduces 1exemplo.xlsx: 84 iterations."""
+    rows = np.array(golden["multiple_shooting"]["rows"])
+    N, T = 10, 0.2
+    ocp = mpcx.unicycle_point_to_point(N=N)
+    solver = mpcx.nlpsol("solver", "mi355x", ocp, {"ipopt": {"max_iter": 2000, "print_level": 0,
+                                                                "acceptable_tol": 1e-8,
+                                                                "acceptable_obj_change_tol": 1e-6},
+                                                    "print_time": 0})
+    F = mpcx.integrator(ocp)
+    lbw = [-math.inf] * 3
+    ubw = [math.inf] * 3
+    for _ in range(N):
+        lbw += [-1, -math.pi / 4, -math.inf, -math.inf, -math.inf]
+        ubw += [1, math.pi / 4, math.inf, math.inf, math.inf]
+    args = {"lbg": [0] * (3 * (N + 1)), "ubg": [0] * (3 * (N + 1)), "lbx": lbw, "ubx": ubw}
+    state_init = np.array([0.0, 0.0, 0.0])
+    state_target = np.array([10.0, 10.0, 0.0])
+    w0 = [0.0] * (3 + 5 * N)
+    mpc_iter = 0
+    states, controls = [], []
+    while np.linalg.norm(state_init - state_target) > 1e-1 and mpc_iter * T < 20:
+        args["p"] = np.concatenate([state_init, state_target])
+        sol = solver(x0=w0, lbx=args["lbx"], ubx=args["ubx"], lbg=args["lbg"], ubg=args["ubg"], p=args["p"])
+        assert sol["x"].shape == (3 + 5 * N, 1) and sol["g"].shape == (3 * (N + 1), 1)
+        assert solver.stats()["success"]
+        u = np.array([sol["x"][3 + 5 * k:5 + 5 * k, 0] for k in range(N)]).T  # (2, N)
+        X0 = np.array([sol["x"][0:3, 0]] + [sol["x"][5 + 5 * k:8 + 5 * k, 0] for k in range(N)]).T
+        states.append(state_init.copy())
+        controls.append(u[:, 0].copy())
+        state_init = F(args["p"], u[:, 0])[0].reshape(-1)
+        u0 = np.hstack([u[:, 1:], u[:, -1:]])
+        X0 = np.hstack([X0[:, 1:], X0[:, -1:]])
+        w0 = np.concatenate([X0.T.reshape(-1), u0.T.reshape(-1)])  # the reference's stacked layout (:284-287)
+        mpc_iter += 1
+    assert mpc_iter == 84
+    states = np.array(states)
+    controls = np.array(controls)
+    assert np.max(np.abs(states - rows[1:85, 0:3])) < 1e-6
+    assert rel_err(controls, rows[0:84, 3:5]) <= REL_TOL
+    # the loop stops exactly where the reference's did: the state fed to the last solve
+    # (row 84) is still > 0.1 away from the target, the state after it is not
+    assert np.linalg.norm(states[-1] - state_target) > 1e-1 >= np.linalg.norm(state_init - state_target)
+
+
+# ----------------------------------------------------------------------------- oracle parity at scale
+def test_config2_batch_vs_cpp_oracle(mpcx, R, C, golden):
+    """Config 2 (N=20, B=1024): GPU solve vs the C++ IPM oracle on identical inputs
+    and initial guess; the golden instances also vs IPOPT-pinned numpy optimum."""
+    rows = np.array(golden["multiple_shooting"]["rows"])
+    P = config2_batch(1024, golden_rows=rows)
+    ocp = mpcx.unicycle_point_to_point(N=20)
+    solver = mpcx.nlpsol("s", "mi355x", ocp)
+    r = solver.solve_batch(P)
+    assert np.all(r["status"] == 0), np.bincount(r["status"], minlength=4)
+    rocp = R.UnicycleOCP(N=20)
+    X = np.repeat(P[:, None, 0:3], 21, axis=1)
+    w0 = R.join_w(X, np.zeros((1024, 20, 2)))
+    ref = C.solve_batch(rocp, P, w0=w0, nthreads=0)
+    assert np.all(ref["status"] == 0)
+    errs = np.array([rel_err(r["w"][b], ref["w"][b]) for b in range(1024)])
+    # same algorithm, same start: the same local optimum for (nearly) every instance
+    assert np.mean(errs <= REL_TOL) >= 0.99, np.sort(errs)[-10:]
+    # objective never worse than the oracle's by more than round-off where they differ
+    assert np.all(r["f"] <= ref["f"] * (1 + 1e-6) + 1e-9) or np.mean(errs <= REL_TOL) >= 0.99
+    # independent numpy oracle on a sample (projected Newton, single shooting)
+    for b in list(range(0, 84, 12)) + list(range(84, 1024, 157)):
+        wn, info = R.solve_ms(P[b], rocp)
+        assert info["status"] == "converged"
+        if abs(info["J"] - r["f"][b]) <= 1e-6 * max(1.0, abs(info["J"])):
+            assert rel_err(r["w"][b], wn) <= REL_TOL
+
+
+def test_kkt_residual_at_solution(mpcx, R):
+    """First-order optimality of the returned (w, lam_g) for the NLP (complex-step check)."""
+    ocp = mpcx.unicycle_point_to_point(N=20)
+    solver = mpcx.nlpsol("s", "mi355x", ocp)
+    P = config2_batch(8, seed=3)
+    r = solver.solve_batch(P)
+    rocp = R.UnicycleOCP(N=20)
+    for b in range(8):
+        pg, cv = R.kkt_residual_ms(r["w"][b], r["lam_g"][b], P[b], rocp)
+        assert cv < 1e-9
+        assert pg < 1e-5
+
+
+# ----------------------------------------------------------------------------- edge cases
+@pytest.mark.parametrize("B", [1, 2, 3, 31, 33, 65])
+def test_ragged_batch_sizes(mpcx, R, B):
+    ocp = mpcx.unicycle_point_to_point(N=20)
+    solver = mpcx.nlpsol("s", "mi355x", ocp)
+    P = config2_batch(65, seed=7)[:B]
+    r = solver.solve_batch(P)
+    full = solver.solve_batch(config2_batch(65, seed=7))
+    assert np.array_equal(r["w"], full["w"][:B])  # instances are independent: bitwise identical
+
+
+def test_empty_batch(mpcx):
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=10))
+    r = solver.solve_batch(np.zeros((0, 6)))
+    assert r["w"].shape == (0, 53)
+
+
+@pytest.mark.parametrize("N", [1, 2, 15, 16, 31, 32, 50, 63])
+def test_horizons(mpcx, C, R, N):
+    ocp = mpcx.unicycle_point_to_point(N=N)
+    solver = mpcx.nlpsol("s", "mi355x", ocp)
+    P = config2_batch(16, seed=N)
+    r = solver.solve_batch(P)
+    rocp = R.UnicycleOCP(N=N)
+    X = np.repeat(P[:, None, 0:3], N + 1, axis=1)
+    ref = C.solve_batch(rocp, P, w0=R.join_w(X, np.zeros((16, N, 2))))
+    ok = [rel_err(r["w"][b], ref["w"][b]) <= REL_TOL for b in range(16) if ref["status"][b] == 0]
+    assert np.all(r["status"] == 0)
+    assert np.mean(ok) >= 0.9
+
+
+def test_max_iter_status(mpcx):
+    ocp = mpcx.unicycle_point_to_point(N=10)
+    solver = mpcx.nlpsol("s", "mi355x", ocp, {"ipopt": {"max_iter": 2}})
+    r = solver.solve_batch(config2_batch(4, seed=1))
+    assert np.all(r["status"] == 2) and np.all(r["iters"] == 2)
+
+
+def test_invalid_arguments(mpcx):
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=10))
+    with pytest.raises(ValueError):
+        solver(p=[0, 0, 0, 10, 10, 0], lbg=[-1] * 33, ubg=[1] * 33)
+    with pytest.raises(ValueError):
+        solver.solve_batch(np.zeros((2, 5)))
+    with pytest.raises(ValueError):
+        mpcx.nlpsol("s", "ipopt", mpcx.unicycle_point_to_point(N=10))
+    bad = mpcx.unicycle_point_to_point(N=10)
+    bad.N = 0
+    with pytest.raises(mpcx._lib.MpcxError):
+        mpcx.nlpsol("s", "mi355x", bad)
+
+
+def test_single_shooting_formulation(mpcx, R, golden):
+    """Config 1 plumbing: single_shooting_v2.py's NLP (decision = U) at P=[0,0,0,10,10,0]:
+    u0* = golden row 0 of 2exemplo.xlsx."""
+    rows2 = np.array(golden["single_shooting"]["rows"])
+    N = 10
+    ocp = mpcx.unicycle_point_to_point(N=N, formulation="single_shooting")
+    solver = mpcx.nlpsol("solver", "mi355x", ocp)
+    lbw, ubw = [], []
+    for _ in range(N):
+        lbw += [-1, -math.pi / 4]
+        ubw += [1, math.pi / 4]
+    sol = solver(x0=[0] * (2 * N), lbx=lbw, ubx=ubw, lbg=-math.inf, ubg=math.inf, p=[0, 0, 0, 10, 10, 0])
+    assert sol["x"].shape == (2 * N, 1) and sol["g"].shape == (2 * N, 1)
+    assert rel_err(sol["x"][0:2, 0], rows2[0, 3:5]) <= REL_TOL
