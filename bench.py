@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Benchmark: batched receding-horizon MPC solves on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload: the closed loop of
+Casadi/multiple_shooting_casadi.py:224-298 for B = 1024 independent instances per
+GPU (unicycle, multiple shooting, N = 20, RK4 M = 4, quadrature cost), inputs
+from the config-2 generator (global instances 0..83 = the golden P_j).  One
+step = one batched NLP solve of all B instances to IPOPT tolerance (1e-8,
+warm-started from the previous step's shifted solution; the first warmup step
+is cold) + the plant/shift update, all on the device.  Weak scaling: every rank
+owns B instances; no collective inside the timed region.
+
+Printed JSON (rank 0): value = total solves/s over all ranks; ms_per_step = the
+max-over-ranks wall time per step; ms_per_solve_p50 = median batched solve-call
+latency (HIP events).  `roofline` describes the RK4 + Jacobian sweep kernel
+(rk4_sens, the HBM-streaming kernel of SURVEY.md §8(d)) at B = 2^19, N = 20;
+`cpu_baseline` times the C++ CPU oracle (oracle/ipm_ref.cpp, kind "port") on
+host cores on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mpc-verde_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "MPC solves/sec (batched) + ms/solve p50, unicycle N=20 at 1/2/4/8 MI355X"
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SWEEP_BYTES_PER_STAGE = 256  # read x_k,u_k,x_{k+1} (64 B) + write c,q,A,B,grad q (192 B)
+SWEEP_BYTES_PER_INSTANCE = 48  # P
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1024, help="instances per GPU")
+    ap.add_argument("--N", type=int, default=20)
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--roofline-batch", type=int, default=1 << 19)
+    ap.add_argument("--roofline-reps", type=int, default=20)
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=4)
+    ap.add_argument("--profile-sweep-only", action="store_true", help="only launch the sweep (for rocprofv3 --pmc)")
+    return ap.parse_args()
+
+
+def shift_np(w, N):
+    """Host copy of shift_kernel's warm start: X_k <- X_{k+1}, U_k <- U_{k+1}, last repeated."""
+    w0 = np.empty_like(w)
+    ix = lambda k: slice(0, 3) if k == 0 else slice(5 + 5 * (k - 1), 8 + 5 * (k - 1))  # noqa: E731
+    for k in range(N + 1):
+        w0[:, ix(k)] = w[:, ix(min(k + 1, N))]
+        if k < N:
+            su = min(k + 1, N - 1)
+            w0[:, 3 + 5 * k:5 + 5 * k] = w[:, 3 + 5 * su:5 + 5 * su]
+    return w0
+
+
+def cpu_baseline(P0, N, steps, cores):
+    """C++ oracle (port of the same NLP + IPOPT-style IPM) on host cores: `steps`
+    closed-loop steps of the same instances, solve calls timed."""
+    from oracle import ipm_ref, nlp_ref
+
+    ipm_ref.build()
+    ocp = nlp_ref.UnicycleOCP(N=N)
+    P = P0.copy()
+    B = P.shape[0]
+    w0 = None
+    t_solve = 0.0
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        r = ipm_ref.solve_batch(ocp, P, w0=w0 if w0 is not None else _cold(P, N, nlp_ref), nthreads=cores)
+        t_solve += time.perf_counter() - t0
+        xf, _ = nlp_ref.F(P[:, 0:3], r["w"][:, 3:5], P[:, 3:6], ocp)
+        P[:, 0:3] = xf
+        w0 = shift_np(r["w"], N)
+    return B * steps / t_solve, t_solve
+
+
+def _cold(P, N, nlp_ref):
+    X = np.repeat(P[:, None, 0:3], N + 1, axis=1)
+    return nlp_ref.join_w(X, np.zeros((P.shape[0], N, 2)))
+
+
+def sweep_roofline(solver, torch, B, N, reps, stream):
+    """Time the rk4_sens sweep kernel at B instances (SoA buffers resident in HBM)."""
+    from mpcx import _lib
+    import ctypes
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device="cpu").manual_seed(7)
+    X = torch.empty(((N + 1) * 3, B), dtype=torch.float64)
+    X[0::3].uniform_(-10, 10, generator=g)
+    X[1::3].uniform_(-10, 10, generator=g)
+    X[2::3].uniform_(-3.14, 3.14, generator=g)
+    U = torch.empty((N * 2, B), dtype=torch.float64).uniform_(-0.78, 0.78, generator=g)
+    XR = torch.empty((3, B), dtype=torch.float64).uniform_(-10, 10, generator=g)
+    X, U, XR = X.to(dev), U.to(dev), XR.to(dev)
+    outs = [torch.empty((N * m, B), dtype=torch.float64, device=dev) for m in (3, 1, 9, 6, 5)]
+    lib = _lib.load()
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    s = ctypes.c_void_p(stream.cuda_stream)
+
+    def launch():
+        _lib.check(lib.mpcx_rk4_sens_dev(solver._h.ptr, B, vp(X), vp(U), vp(XR), *[vp(o) for o in outs], s))
+
+    for _ in range(3):
+        launch()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        launch()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del X, U, XR, outs
+    torch.cuda.empty_cache()
+    return ms
+
+
+def load_traffic(B, N):
+    """HBM bytes per sweep launch from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "rk4_sens_pmc.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("B") == B and d.get("N") == N:
+            return float(d["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    args = parse()
+    from mpcx import dist as mdist
+
+    rank, world, local = mdist.env()
+    import torch
+
+    torch.cuda.set_device(local)
+    mdist.init("nccl")
+    import mpcx
+    from mpcx.device import DeviceLoop
+
+    N, B = args.N, args.batch
+    ocp = mpcx.unicycle_point_to_point(N=N)
+    solver = mpcx.nlpsol("bench", "mi355x", ocp, {"ipopt": {"max_iter": 3000}}, device=local)
+    stream = torch.cuda.current_stream()
+
+    if args.profile_sweep_only:
+        ms = sweep_roofline(solver, torch, args.roofline_batch, N, args.roofline_reps, stream)
+        if rank == 0:
+            print(json.dumps({"sweep_ms": ms, "B": args.roofline_batch, "N": N}))
+        return
+
+    start, stop = mdist.shard(B, rank)
+    P0 = mdist.config2_inputs(start, stop, args.seed)
+    loop = DeviceLoop(solver, P0, device=f"cuda:{local}", stream=stream)
+
+    for _ in range(args.warmup):
+        loop.step()
+    torch.cuda.synchronize()
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    iters_hist = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
+    status_hist = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        ev[i][0].record(stream)
+        loop.solve(status_out=status_hist[i], iters_out=iters_hist[i])
+        ev[i][1].record(stream)
+        loop.shift()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = mdist.max_over_ranks(t1 - t0, device=loop.P.device)
+    solve_ms = sorted(a.elapsed_time(b) for a, b in ev)
+    p50 = mdist.max_over_ranks(float(np.median(solve_ms)), device=loop.P.device)
+
+    # closed-loop statistics: the only collective (RCCL all_gather over xGMI), outside the timed region
+    P_fin = loop.P.cpu().numpy()
+    S = mdist.stats_matrix(P_fin, None, loop.f.cpu().numpy(), status_hist.max(dim=0).values.cpu().numpy(),
+                           iters_hist.cpu().numpy())
+    S_all = mdist.all_gather_stats(S, device=loop.P.device)
+    iters_max_step = mdist.max_over_ranks(float(iters_hist.max(dim=1).values.double().mean().item()),
+                                          device=loop.P.device)
+
+    roof = None
+    if rank == 0 and not args.no_roofline:
+        Br = args.roofline_batch
+        ms = sweep_roofline(solver, torch, Br, N, args.roofline_reps, stream)
+        alg = Br * (SWEEP_BYTES_PER_STAGE * N + SWEEP_BYTES_PER_INSTANCE)
+        ach = alg / (ms * 1e-3) / 1e9
+        traffic = load_traffic(Br, N)
+        roof = {"kernel": "rk4_sens_kernel (RK4 M=4 + Jacobian sweep)", "bound": "hbm", "achieved": round(ach, 1),
+                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic,
+                "launch_ms": round(ms, 4), "units_per_launch": Br * N, "unit_of_work": "stage evaluation",
+                "bytes_per_launch": alg, "config": f"B={Br}, N={N}"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        cores = max(1, min(cores, os.cpu_count() or 1))
+        rate, t = cpu_baseline(P0, N, args.cpu_steps, cores)
+        cpu = {"value": round(rate, 1), "unit": "solves/s", "cores": cores, "kind": "port",
+               "sample": f"{args.cpu_steps} closed-loop steps x {B} config-2 instances (N={N}), solve calls timed, "
+                         f"{t:.1f} s wall"}
+
+    if rank == 0:
+        total = world * B * K
+        out = {
+            "metric": METRIC, "value": round(total / elapsed, 1), "unit": "solves/s", "n_gpus": world,
+            "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),
+            "ms_per_solve_p50": round(p50, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: SURVEY config-2 generator (global instances 0-83 = golden P_j of Casadi/1exemplo.xlsx)",
+            "config": {"workload": "config 2: closed-loop point-to-point MPC, unicycle, multiple shooting N=20, "
+                                   "RK4 M=4 quadrature cost, IPOPT tol 1e-8", "dynamics": "unicycle", "N": N,
+                       "M": 4, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"instance-sharded x{world} (no data-path collective)"},
+            "iters_mean": round(float(S_all[:, 1].mean()), 2), "iters_max": int(S_all[:, 2].max()),
+            "iters_max_per_step_mean": round(float(iters_max_step), 2),
+            "failed_instances": int((S_all[:, 3] > 1).sum()),
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

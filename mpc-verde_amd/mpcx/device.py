@@ -48,12 +48,17 @@ class DeviceLoop:
         self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
         self._cold = cold_first
 
-    def solve(self):
+    def solve(self, status_out=None, iters_out=None):
+        """Enqueue one batched solve.  status_out / iters_out: optional int32 device
+        tensors (B,) that receive this step's statuses / iteration counts directly
+        from the kernel (no extra launch)."""
         lib = _lib.load()
         s = ctypes_void(self.stream.cuda_stream)
         w0 = None if self._cold else _ptr(self.w0)
+        st = self.status if status_out is None else status_out
+        it = self.iters if iters_out is None else iters_out
         _lib.check(lib.mpcx_solve_batch_dev(self.solver._h.ptr, self.B, _ptr(self.P), w0, _ptr(self.w),
-                                            _ptr(self.f), None, _ptr(self.status), _ptr(self.iters), s))
+                                            _ptr(self.f), None, _ptr(st), _ptr(it), s))
         self._cold = False
 
     def shift(self):

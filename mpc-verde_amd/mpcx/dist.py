@@ -1,0 +1,111 @@
+"""One process per GPU: instance sharding and closed-loop statistics collection.
+
+MPC instances (initial state x reference) are independent for the whole closed
+loop, so the data path has NO collective: rank r owns the
+contiguous block of global instance ids [r*B, (r+1)*B) (weak scaling) and
+builds its own inputs from (seed, global id).  The only communication is one
+``all_gather`` of per-instance statistics after the loop -- RCCL over xGMI with
+the ``nccl`` backend on ROCm, ``gloo`` on CPU (tests).
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+STAT_FIELDS = ("final_error", "iters_mean", "iters_max", "status_max", "f_last", "x", "y", "theta")
+
+
+def env():
+    """(rank, world_size, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(backend: str):
+    import torch.distributed as dist
+
+    rank, world, _ = env()
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return rank, world
+
+
+def shard(B_per_rank: int, rank: int):
+    return rank * B_per_rank, (rank + 1) * B_per_rank
+
+
+def _golden_P(path=None):
+    if path is None:
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        path = os.path.join(root, "tests", "golden", "unicycle_N10_golden.json")
+    if not os.path.exists(path):
+        return np.zeros((0, 6))
+    with open(path) as f:
+        rows = np.array(json.load(f)["multiple_shooting"]["rows"], float)
+    n = rows.shape[0] - 1
+    P = np.zeros((n, 6))
+    P[:, 0:3] = rows[1:, 0:3]
+    P[:, 3:6] = (10.0, 10.0, 0.0)
+    return P
+
+
+def config2_inputs(start: int, stop: int, seed: int = 20261015, with_golden=True):
+    """global instances 0..83 are the 84 recorded golden
+    P_j (Casadi/1exemplo.xlsx); the rest x, y ~ U[-5, 5], th ~ U[-pi/2, pi/2],
+    target (10, 10, 0).  Instance g's draw depends only on (seed, g)."""
+    n = stop - start
+    P = np.zeros((n, 6))
+    P[:, 3:6] = (10.0, 10.0, 0.0)
+    for i, g in enumerate(range(start, stop)):
+        r = np.random.default_rng([seed, g]).uniform(size=3)
+        P[i, 0:2] = -5.0 + 10.0 * r[0:2]
+        P[i, 2] = -np.pi / 2 + np.pi * r[2]
+    if with_golden:
+        Pg = _golden_P()
+        lo, hi = start, min(stop, Pg.shape[0])
+        if hi > lo:
+            P[0:hi - lo] = Pg[lo:hi]
+    return P
+
+
+def stats_matrix(P, w, f, status, iters_hist):
+    """Per-instance closed-loop statistics, (B, len(STAT_FIELDS)) float64."""
+    B = P.shape[0]
+    it = np.asarray(iters_hist, float).reshape(-1, B) if len(iters_hist) else np.zeros((1, B))
+    S = np.zeros((B, len(STAT_FIELDS)))
+    S[:, 0] = np.linalg.norm(P[:, 0:3] - P[:, 3:6], axis=1)
+    S[:, 1] = it.mean(axis=0)
+    S[:, 2] = it.max(axis=0)
+    S[:, 3] = np.asarray(status, float)
+    S[:, 4] = np.asarray(f, float)
+    S[:, 5:8] = P[:, 0:3]
+    return S
+
+
+def all_gather_stats(S_local, device=None):
+    """Gather every rank's (B, F) statistics block on every rank (RCCL/gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return np.asarray(S_local)
+    t = torch.as_tensor(np.ascontiguousarray(S_local), dtype=torch.float64)
+    if device is not None:
+        t = t.to(device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return torch.cat(out).cpu().numpy()
+
+
+def max_over_ranks(x: float, device=None):
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(x)
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
