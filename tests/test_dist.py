@@ -1,0 +1,94 @@
+"""CPU: the multi-GPU path (instance sharding, per-rank inputs, stats all_gather,
+max-over-ranks timing) with world_size = 2 on the gloo backend.
+
+The per-rank solver here is the C++ CPU oracle (the GPU is exercised by the
+gpu tests and by bench.py); what is tested is that a sharded run reproduces the
+single-process run instance-for-instance and that the collectives assemble it.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _closed_loop_shard(P, steps, N):
+    from oracle import ipm_ref, nlp_ref
+
+    ocp = nlp_ref.UnicycleOCP(N=N)
+    X = np.repeat(P[:, None, 0:3], N + 1, axis=1)
+    w0 = nlp_ref.join_w(X, np.zeros((P.shape[0], N, 2)))
+    iters = []
+    P = P.copy()
+    import bench
+
+    for _ in range(steps):
+        r = ipm_ref.solve_batch(ocp, P, w0=w0, nthreads=1)
+        iters.append(r["iters"])
+        P[:, 0:3], _ = nlp_ref.F(P[:, 0:3], r["w"][:, 3:5], P[:, 3:6], ocp)
+        w0 = bench.shift_np(r["w"], N)
+    return P, r, np.array(iters)
+
+
+def _worker(rank, world, port, B, steps, N, out):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    from mpcx import dist
+
+    r, w = dist.init("gloo")
+    assert (r, w) == (rank, world)
+    start, stop = dist.shard(B, rank)
+    P = dist.config2_inputs(start, stop)
+    Pf, res, iters = _closed_loop_shard(P, steps, N)
+    S = dist.stats_matrix(Pf, res["w"], res["f"], res["status"], iters)
+    S_all = dist.all_gather_stats(S)
+    tmax = dist.max_over_ranks(float(rank + 1))
+    if rank == 0:
+        out.put((S_all, tmax))
+    import torch.distributed as tdist
+
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def test_config2_inputs_are_shard_invariant():
+    from mpcx import dist
+
+    full = dist.config2_inputs(0, 256)
+    parts = [dist.config2_inputs(*dist.shard(64, r)) for r in range(4)]
+    assert np.array_equal(np.concatenate(parts), full)
+    assert np.all(np.abs(full[84:, 0:2]) <= 5) and np.all(np.abs(full[84:, 2]) <= np.pi / 2)
+    assert np.array_equal(full[:84], dist._golden_P())
+
+
+@pytest.mark.timeout(300)
+def test_world_size_2_gloo_matches_single_process():
+    from mpcx import dist
+
+    B, steps, N, world = 16, 2, 20, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, steps, N, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    S_all, tmax = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert S_all.shape == (world * B, len(dist.STAT_FIELDS))
+    assert tmax == 2.0
+    # single-process reference over the same 2B global instances
+    P = dist.config2_inputs(0, world * B)
+    Pf, res, iters = _closed_loop_shard(P, steps, N)
+    S_ref = dist.stats_matrix(Pf, res["w"], res["f"], res["status"], iters)
+    assert np.array_equal(S_all, S_ref)  # independent instances: bitwise identical

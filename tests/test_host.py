@@ -1,0 +1,123 @@
+"""CPU: the C-ABI library loads and exports every symbol include/mpcx.h declares;
+host-side logic of the façade; the product never imports the oracle."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "mpc-verde_amd", "mpcx", "libmpcx.so")
+HDR = os.path.join(ROOT, "include", "mpcx.h")
+
+
+def declared_symbols():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(mpcx_\w+)\s*\(", src, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "mpc-verde_amd")], check=True)
+    return ctypes.CDLL(LIB)
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for s in ("mpcx_create", "mpcx_solve_batch", "mpcx_solve_batch_dev", "mpcx_plant_step", "mpcx_rk4_sens",
+              "mpcx_destroy", "mpcx_last_error"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol(lib):
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    for s in declared_symbols():
+        assert re.search(rf"\bT {s}$", out, re.M), s
+
+
+def test_library_targets_gfx950():
+    """The shared library embeds a gfx950 code object (HIP fat binary)."""
+    data = open(LIB, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data or b"gfx950" in data
+
+
+def test_python_binding_matches_header():
+    import mpcx
+
+    assert set(mpcx._lib.EXPORTS) == set(declared_symbols())
+    # struct layout: 8 int32 + 2 double + 6 x double[8]
+    assert ctypes.sizeof(mpcx._lib.Spec) == 8 * 4 + 2 * 8 + 6 * 8 * 8
+
+
+def test_default_spec_without_gpu(lib):
+    import mpcx
+
+    s = mpcx._lib.Spec()
+    assert lib.mpcx_default_spec(ctypes.byref(s), 1, 20) == 0
+    assert s.N == 20 and s.M == 4 and abs(s.T - 0.2) < 1e-15 and s.max_iter == 2000
+    assert list(s.Q[:3]) == [1.0, 5.0, 0.1] and list(s.R[:2]) == [0.5, 0.05]
+    assert lib.mpcx_default_spec(ctypes.byref(s), 99, 20) < 0
+
+
+def test_no_cpu_fallback_when_gpu_missing():
+    """The product path fails loudly without a HIP device (no silent CPU path)."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    import mpcx
+
+    with pytest.raises(mpcx._lib.MpcxError):
+        mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=10))
+
+
+def test_to_spec_mirrors_reference_constants():
+    import mpcx
+
+    s = mpcx.to_spec(mpcx.unicycle_point_to_point(N=20))
+    assert (s.N, s.M, s.cost, s.param_layout) == (20, 4, 0, 0)
+    assert s.lbu[0] == -1.0 and s.ubu[1] == pytest.approx(np.pi / 4)
+    assert s.lbx[0] == -1e20 and s.ubx[2] == 1e20
+    t = mpcx.to_spec(mpcx.unicycle_tracking(N=30))
+    assert (t.N, t.M, t.cost, t.param_layout) == (30, 1, 1, 1)
+    assert (t.lbx[0], t.ubx[0], t.lbx[1], t.ubx[1]) == (-20.0, 20.0, -2.0, 2.0)
+
+
+def test_vec_coercion():
+    from mpcx.nlpsol import _vec
+
+    assert np.array_equal(_vec(3.0, 4, "a"), np.full(4, 3.0))
+    assert np.array_equal(_vec([[1], [2]], 2, "a"), np.array([1.0, 2.0]))
+    with pytest.raises(ValueError):
+        _vec([1, 2, 3], 2, "a")
+
+
+def test_product_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "mpc-verde_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                src = open(os.path.join(dp, f)).read()
+                assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), f
+                assert "ipm_ref" not in src and "nlp_ref" not in src, f
+
+
+def test_shift_matches_reference_receding_horizon():
+    """bench.shift_np == shift_kernel semantics: X_k <- X_{k+1}, U_k <- U_{k+1}, tail repeated
+    (Casadi/multiple_shooting_casadi.py:274-283, interleaved layout)."""
+    import bench
+    from oracle import nlp_ref
+
+    N = 4
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(2, N + 1, 3))
+    U = rng.normal(size=(2, N, 2))
+    w0 = bench.shift_np(nlp_ref.join_w(X, U), N)
+    X2, U2 = nlp_ref.split_w(w0, N)
+    assert np.array_equal(X2[:, :N], X[:, 1:]) and np.array_equal(X2[:, N], X[:, N])
+    assert np.array_equal(U2[:, :N - 1], U[:, 1:]) and np.array_equal(U2[:, N - 1], U[:, N - 1])

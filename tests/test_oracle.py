@@ -1,0 +1,147 @@
+"""CPU: pin the oracles against the reference's own outputs (tests/golden).
+
+Golden data = Casadi/1exemplo.xlsx (multiple shooting, CasADi+IPOPT) and
+Casadi/2exemplo.xlsx (single shooting) decoded by tests/golden/make_golden.py.
+"""
+import numpy as np
+import pytest
+
+from oracle import ipm_ref, nlp_ref as R
+
+REL_TOL = 1e-4
+
+
+def rel_err(a, b):
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b))) / max(float(np.max(np.abs(b))), 1e-3))
+
+
+@pytest.fixture(scope="module")
+def rows(golden):
+    return np.array(golden["multiple_shooting"]["rows"])
+
+
+def test_golden_fixture_shape(golden):
+    for key in ("multiple_shooting", "single_shooting"):
+        r = np.array(golden[key]["rows"])
+        assert r.shape == (85, 6)
+        assert np.all(r[0, 0:3] == 0) and np.allclose(r[0, 3:5], [1.0, np.pi / 4])
+
+
+def test_golden_spread(golden):
+    """The two reference formulations agree only to IPOPT's tolerance."""
+    a = np.array(golden["multiple_shooting"]["rows"])
+    b = np.array(golden["single_shooting"]["rows"])
+    assert np.max(np.abs(a[:, 0:3] - b[:, 0:3])) < 3e-8
+    assert np.max(np.abs(a[:, 3:5] - b[:, 3:5])) < 2e-7
+
+
+def test_plant_replays_golden_exactly(rows):
+    """RK4-M4 F (multiple_shooting_casadi.py:98-114) reproduces every recorded transition."""
+    ocp = R.UnicycleOCP()
+    xf, _ = R.F(rows[1:-1, 0:3], rows[:-2, 3:5], np.array([10.0, 10.0, 0.0]), ocp)
+    assert np.max(np.abs(xf - rows[2:, 0:3])) < 1e-14
+
+
+def test_numpy_oracle_golden_pairs(rows):
+    """Projected-Newton single-shooting oracle reproduces the 84 IPOPT u0* (every 3rd pair)."""
+    P, U0 = R.golden_pairs(rows)
+    ocp = R.UnicycleOCP()
+    for j in range(0, 84, 3):
+        U, X, info = R.solve_single_shooting(P[j], ocp)
+        assert info["status"] == "converged"
+        assert rel_err(U[0], U0[j]) <= 1e-5
+
+
+def test_numpy_oracle_closed_loop(rows):
+    """Replay of the reference's closed loop: 84 iterations, states within IPOPT tolerance."""
+    cl = R.closed_loop(R.UnicycleOCP())
+    assert cl["iterations"] == 84
+    assert np.max(np.abs(cl["states"][:84] - rows[1:, 0:3])) < 1e-7
+    assert np.max(np.abs(cl["controls"] - rows[:84, 3:5])) < 1e-6
+
+
+def test_complex_step_jacobian_vs_central_differences():
+    ocp = R.UnicycleOCP()
+    rng = np.random.default_rng(0)
+    x, u, xr = rng.normal(size=3), rng.normal(size=2), rng.normal(size=3)
+    J = R.stage_jacobian(x, u, xr, ocp)
+    z = np.concatenate([x, u])
+    Jfd = np.zeros((4, 5))
+    for b in range(5):
+        e = np.zeros(5)
+        e[b] = 1e-6
+        xp, qp = R.F((z + e)[0:3], (z + e)[3:5], xr, ocp)
+        xm, qm = R.F((z - e)[0:3], (z - e)[3:5], xr, ocp)
+        Jfd[:, b] = (np.append(xp, qp) - np.append(xm, qm)) / 2e-6
+    assert np.max(np.abs(J - Jfd)) < 1e-7
+
+
+def test_cpp_oracle_stage_derivatives():
+    """Jet (second-order forward) derivatives of the C++ oracle vs complex step / FD-of-CS."""
+    for cost in ("quadrature", "node"):
+        ocp = R.UnicycleOCP(cost=cost, M=4 if cost == "quadrature" else 1)
+        rng = np.random.default_rng(1)
+        B = 12
+        x, u, xr, lam = (rng.normal(size=(B, 3)), rng.normal(size=(B, 2)), rng.normal(size=(B, 3)),
+                         rng.normal(size=(B, 3)))
+        xf, qf, jac, hess = ipm_ref.stage(ocp, x, u, xr, lam=lam)
+        xf2, qf2 = R.F(x, u, xr, ocp)
+        assert np.max(np.abs(xf - xf2)) < 1e-13 and np.max(np.abs(qf - qf2)) < 1e-12 * max(1, np.abs(qf2).max())
+        assert np.max(np.abs(jac - R.stage_jacobian(x, u, xr, ocp))) < 1e-12
+        H = R.stage_hessians(x, u, xr, ocp)
+        Hl = H[:, 3] + np.einsum("bc,bcij->bij", lam, H[:, 0:3])
+        assert np.max(np.abs(ipm_ref.unpack_sym5(hess) - Hl)) < 1e-7
+
+
+def test_cpp_oracle_golden_pairs(rows):
+    """The C++ IPOPT-style IPM reproduces all 84 recorded IPOPT solves from a cold start."""
+    P, U0 = R.golden_pairs(rows)
+    out = ipm_ref.solve_batch(R.UnicycleOCP(), P, nthreads=4)
+    assert np.all(out["status"] == 0)
+    assert max(rel_err(out["w"][j, 3:5], U0[j]) for j in range(84)) <= 1e-5
+
+
+def test_cpp_oracle_agrees_with_numpy_oracle_N20():
+    """Two independent algorithms, same NLP and start -> same optimum (config 2 sizes)."""
+    from mpcx import dist
+
+    P = dist.config2_inputs(84, 84 + 24, with_golden=False)
+    ocp = R.UnicycleOCP(N=20)
+    X = np.repeat(P[:, None, 0:3], 21, axis=1)
+    w0 = R.join_w(X, np.zeros((P.shape[0], 20, 2)))
+    out = ipm_ref.solve_batch(ocp, P, w0=w0, nthreads=4)
+    assert np.all(out["status"] == 0)
+    agree = 0
+    for b in range(0, P.shape[0], 3):
+        w, info = R.solve_ms(P[b], ocp)
+        assert info["status"] == "converged"
+        agree += rel_err(out["w"][b], w) <= REL_TOL
+    assert agree >= 7  # of 8 sampled; a different local optimum is possible (non-convex NLP)
+
+
+def test_cpp_oracle_kkt():
+    ocp = R.UnicycleOCP(N=10)
+    P = np.array([[1.0, -2.0, 0.3, 10.0, 10.0, 0.0]])
+    out = ipm_ref.solve_batch(ocp, P)
+    pg, cv = R.kkt_residual_ms(out["w"][0], out["lam_g"][0], P[0], ocp)
+    assert cv < 1e-9 and pg < 1e-5
+
+
+def test_tracking_variant_node_cost():
+    """mpctools tracking (Trajectory_tracking.py:51-61): RK4 M=1, node cost l(x_k,u_k,p_k)."""
+    ocp = R.tracking_ocp(N=10)
+    x = np.array([0.1, -0.2, 1.0])
+    u = np.array([0.5, 0.3])
+    p = np.array([1.0, 0.0, np.pi / 2, 1.0, 1.0])
+    xf, q = R.F(x, u, p[0:3], ocp, p[3:5])
+    d = x - p[0:3]
+    du = u - p[3:5]
+    assert abs(q - (d[0] ** 2 + d[1] ** 2 + 0.1 * d[2] ** 2 + 0.5 * du[0] ** 2 + 0.05 * du[1] ** 2)) < 1e-14
+    # one RK4 step of the unicycle
+    h = 0.2
+    f = lambda s: np.array([u[0] * np.cos(s[2]), u[0] * np.sin(s[2]), u[1]])  # noqa: E731
+    k1 = f(x)
+    k2 = f(x + h / 2 * k1)
+    k3 = f(x + h / 2 * k2)
+    k4 = f(x + h * k3)
+    assert np.max(np.abs(xf - (x + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)))) < 1e-15
