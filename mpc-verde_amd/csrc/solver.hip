@@ -600,40 +600,48 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
 }
 
 // ------------------------------------------------------------------------------
-// RK4 + Jacobian sweep: one thread per (interval k, instance b), SoA streams.
-// Reads X_k, U_k, X_{k+1}, xr; writes c_k, q_k, A_k, B_k, grad q_k.
+// RK4 + Jacobian sweep over B x N intervals, structure-of-arrays streams.
+// One thread per instance walks its N intervals: X_{k+1} loaded for interval k
+// stays in registers as interval k+1's X_k and x_ref is loaded once, so HBM sees
+// exactly the compulsory bytes (reads (N+1)*3 + 2N + 3 doubles, writes 24N
+// doubles per instance).  Consecutive lanes = consecutive
+// instances: every load/store of a wave is one contiguous 512-B segment.
 // ------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void rk4_sens_kernel(int B, int N, StageParams sp, const double* __restrict__ X,
                                                        const double* __restrict__ U, const double* __restrict__ XR,
                                                        double* __restrict__ C, double* __restrict__ Qo,
                                                        double* __restrict__ Ao, double* __restrict__ Bo,
                                                        double* __restrict__ Go) {
-  const long total = (long)B * N;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int b = (int)(t % B);
-    const int k = (int)(t / B);
-    double x[3], u[2], xn[3], xr[3];
-    const double ur[2] = {0.0, 0.0};
+  const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const long Bl = B;
+  double x[3], xr[3];
+  const double ur[2] = {0.0, 0.0};
+  const double lz[3] = {0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      x[i] = X[((long)k * 3 + i) * B + b];
-      xn[i] = X[((long)(k + 1) * 3 + i) * B + b];
-      xr[i] = XR[(long)i * B + b];
-    }
+  for (int i = 0; i < 3; ++i) {
+    x[i] = X[i * Bl + b];
+    xr[i] = XR[i * Bl + b];
+  }
+  for (int k = 0; k < N; ++k) {
+    double u[2], xn[3];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) u[i] = U[((long)k * 2 + i) * B + b];
+    for (int i = 0; i < 3; ++i) xn[i] = X[((long)(k + 1) * 3 + i) * Bl + b];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) u[i] = U[((long)k * 2 + i) * Bl + b];
     double xf[3], q, A[9], Bm[6], g[5], H[15];
-    const double lz[3] = {0, 0, 0};
     uni_derivs<false>(sp, x, u, xr, ur, lz, 1.0, xf, q, A, Bm, g, H);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) C[((long)k * 3 + i) * B + b] = xf[i] - xn[i];
-    Qo[(long)k * B + b] = q;
+    for (int i = 0; i < 3; ++i) C[((long)k * 3 + i) * Bl + b] = xf[i] - xn[i];
+    Qo[(long)k * Bl + b] = q;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) Ao[((long)k * 9 + i) * B + b] = A[i];
+    for (int i = 0; i < 9; ++i) Ao[((long)k * 9 + i) * Bl + b] = A[i];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) Bo[((long)k * 6 + i) * B + b] = Bm[i];
+    for (int i = 0; i < 6; ++i) Bo[((long)k * 6 + i) * Bl + b] = Bm[i];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) Go[((long)k * 5 + i) * B + b] = g[i];
+    for (int i = 0; i < 5; ++i) Go[((long)k * 5 + i) * Bl + b] = g[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x[i] = xn[i];
   }
 }
 
@@ -695,9 +703,7 @@ hipError_t launch_solve(const SolveArgs& a, hipStream_t stream) {
 
 hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X, const double* U, const double* XR,
                            double* C, double* Q, double* A, double* Bm, double* G, hipStream_t stream) {
-  const long total = (long)B * N;
-  long blocks = (total + 255) / 256;
-  if (blocks > 65536) blocks = 65536;
+  const long blocks = ((long)B + 255) / 256;
   hipLaunchKernelGGL(rk4_sens_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, B, N, sp, X, U, XR, C, Q, A, Bm,
                      G);
   return hipGetLastError();
