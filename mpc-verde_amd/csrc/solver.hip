@@ -23,6 +23,26 @@
 
 #include "solver.h"
 
+// Diagnostic build only (-DMPCX_STAMPS, `make stamps`): per-phase s_memtime cycle
+// accounting of the solve loop (cdna_hip_programming.md §7 "In-kernel stamps").
+#ifdef MPCX_STAMPS
+__device__ unsigned long long* g_mpcx_stamps = nullptr;
+#define STAMP(p)                                                                          \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    unsigned long long t_;                                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    st_acc[st_ph] += t_ - st_last;                                                        \
+    st_last = t_;                                                                         \
+    st_ph = (p);                                                                          \
+  } while (0)
+#else
+#define STAMP(p) \
+  do {           \
+  } while (0)
+#endif
+
 namespace mpcx {
 
 
@@ -36,28 +56,94 @@ constexpr double kEtaPhi = 1e-8, kGammaAlpha = 0.05;
 constexpr double kDw0 = 1e-4, kDwMin = 1e-20, kDwMax = 1e40, kKwMinus = 1.0 / 3, kKwPlus = 8, kKwPlusBar = 100;
 constexpr double kBoundPush = 1e-2, kBoundFrac = 1e-2, kInfBound = 1e19;
 
-// ---- lane-group collectives (width G, aligned groups) ----------------------
+// ---- lane-group collectives (width G, aligned groups), all VALU ---------------
+// Neighbour moves are DPP wave shifts; all-reduces are DPP within a 16-lane row
+// (quad_perm xor1, quad_perm xor2, row_half_mirror, row_mirror) followed by
+// v_permlane16_swap / v_permlane32_swap across rows (gfx950).  Every combine is
+// symmetric (a+b on one lane, b+a on its partner), so all lanes of a group end
+// with bit-identical results and take identical control decisions.
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int kQuadXor1 = 0xb1, kQuadXor2 = 0x4e, kHalfMirror = 0x141, kMirror = 0x140;
+constexpr int kWaveShl1 = 0x130, kWaveShr1 = 0x138;
+
+// other 16-lane row of a 32-lane half (xor 16) and other half of the wave (xor 32):
+// the swap builtins hand back both rows; combining p[0] and p[1] in a fixed order
+// keeps the result symmetric.
+struct Pair {
+  double a, b;
+};
+__device__ __forceinline__ Pair rows16(double v) {
+  const long long x = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane16_swap((int)(x & 0xffffffffLL), (int)(x & 0xffffffffLL), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((int)(x >> 32), (int)(x >> 32), false, false);
+  return {__longlong_as_double(((long long)hi[0] << 32) | (unsigned int)lo[0]),
+          __longlong_as_double(((long long)hi[1] << 32) | (unsigned int)lo[1])};
+}
+__device__ __forceinline__ Pair halves32(double v) {
+  const long long x = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((int)(x & 0xffffffffLL), (int)(x & 0xffffffffLL), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((int)(x >> 32), (int)(x >> 32), false, false);
+  return {__longlong_as_double(((long long)hi[0] << 32) | (unsigned int)lo[0]),
+          __longlong_as_double(((long long)hi[1] << 32) | (unsigned int)lo[1])};
+}
+
+struct OpSum {
+  __device__ static double f(double a, double b) { return a + b; }
+};
+struct OpMax {
+  __device__ static double f(double a, double b) { return fmax(a, b); }
+};
+struct OpMin {
+  __device__ static double f(double a, double b) { return fmin(a, b); }
+};
+
+template <int G, class Op>
+__device__ __forceinline__ double greduce(double v) {
+  v = Op::f(v, dpp<kQuadXor1>(v));
+  v = Op::f(v, dpp<kQuadXor2>(v));
+  v = Op::f(v, dpp<kHalfMirror>(v));
+  v = Op::f(v, dpp<kMirror>(v));
+  if (G >= 32) {
+    const Pair p = rows16(v);
+    v = Op::f(p.a, p.b);
+  }
+  if (G >= 64) {
+    const Pair p = halves32(v);
+    v = Op::f(p.a, p.b);
+  }
+  return v;
+}
 template <int G>
 __device__ __forceinline__ double gsum(double v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, G);
-  return __shfl(v, 0, G);  // identical bits on every lane of the group
+  return greduce<G, OpSum>(v);
 }
 template <int G>
 __device__ __forceinline__ double gmax(double v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, G));
-  return v;
+  return greduce<G, OpMax>(v);
 }
 template <int G>
 __device__ __forceinline__ double gmin(double v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, G));
-  return v;
+  return greduce<G, OpMin>(v);
 }
-template <int G>
-__device__ __forceinline__ double from(double v, int src) {  // value of lane `src` of my group
-  return __shfl(v, src, G);
+// value of lane k+1 / k-1 (whole-wave DPP shift; groups are contiguous and the
+// lanes that would read across a group boundary never use the value)
+__device__ __forceinline__ double from_next(double v) { return dpp<kWaveShl1>(v); }
+__device__ __forceinline__ double from_prev(double v) { return dpp<kWaveShr1>(v); }
+
+// 1/x to full fp64 accuracy: v_rcp_f64 + two Newton steps (no IEEE division sequence
+// on the Riccati critical path)
+__device__ __forceinline__ double rcp64(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
 }
 
 __device__ __forceinline__ int ixw(int k, int i) { return k == 0 ? i : 3 + 5 * (k - 1) + 2 + i; }  // X_k[i] in w
@@ -106,7 +192,7 @@ __device__ __forceinline__ bool riccati_step(const double H[15], const double gp
   const double a = Huu[0], b = Huu[1], d = Huu[2];
   const double det = a * d - b * b;
   const bool ok = (a > 0.0) && (det > 0.0) && (d - b * b / a > 0.0);
-  const double id = 1.0 / det;
+  const double id = rcp64(det);
   const double i00 = d * id, i01 = -b * id, i11 = a * id;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
@@ -218,26 +304,22 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
     double ln[3], xn[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      ln[i] = from<G>(lam[i], k + 1);
-      xn[i] = from<G>(z[i], k + 1);
+      ln[i] = from_next(lam[i]);
+      xn[i] = from_next(z[i]);
     }
-    if (hasU) {
+    {
+      // every lane evaluates (SIMD: no extra cost); lanes without an interval mask
+      // the results.  A and B keep their structural 0/1 entries as constants.
       const double u2[2] = {z[3], z[4]};
       uni_derivs<true>(sp, z, u2, xr, ur, ln, fs, xf, qv, A, Bm, gq, Hs);
+      const double m = hasU ? 1.0 : 0.0;
+      qv *= m;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) cdef[i] = xf[i] - xn[i];
-    } else {
-      qv = 0;
+      for (int i = 0; i < 15; ++i) Hs[i] *= m;
 #pragma unroll
-      for (int i = 0; i < 15; ++i) Hs[i] = 0;
+      for (int i = 0; i < 5; ++i) gq[i] *= m;
 #pragma unroll
-      for (int i = 0; i < 5; ++i) gq[i] = 0;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) A[i] = 0;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) Bm[i] = 0;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) cdef[i] = 0;
+      for (int i = 0; i < 3; ++i) cdef[i] = hasU ? xf[i] - xn[i] : 0.0;
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) c0[i] = (valid && k == 0) ? x0[i] - z[i] : 0.0;
@@ -270,11 +352,18 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
   double dz[5], dlam[3], dzL[5], dzU[5];
   double Pk[6], pk[3], Kk[6], kfk[2];
 
+#ifdef MPCX_STAMPS
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_last = 0;
+  int st_ph = 9;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+#endif
   for (it = 0; it <= a.max_iter; ++it) {
+    STAMP(0);
     // ------------------------------------------------------------ optimality error
     double ln[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) ln[i] = from<G>(lam[i], k + 1);
+    for (int i = 0; i < 3; ++i) ln[i] = from_next(lam[i]);
     double Ed = 0, Ecomp0 = 0, Ec = 0, lam1 = 0, z1 = 0;
     double rd[5];
 #pragma unroll
@@ -319,6 +408,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
     }
     if (__all(done)) break;
 
+    STAMP(1);
     // ------------------------------------------------------------ barrier update
     for (int rep = 0; rep < 32; ++rep) {
       double Ecm = 0;
@@ -339,6 +429,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       if (!__any(dec && it == 0)) break;
     }
 
+    STAMP(2);
     // ------------------------------------------------------------ barrier gradient, Sigma
     double sig[5], gp[5];
 #pragma unroll
@@ -357,6 +448,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       }
     }
 
+    STAMP(3);
     // ------------------------------------------------------------ Riccati + inertia correction
     double delta = 0.0;
     bool need = !done;  // instance still needs a factorisation
@@ -378,9 +470,9 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       for (int j = N - 1; j >= 0; --j) {
         double Pin[6], pin[3];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) Pin[i] = from<G>(P[i], k + 1);
+        for (int i = 0; i < 6; ++i) Pin[i] = from_next(P[i]);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) pin[i] = from<G>(p[i], k + 1);
+        for (int i = 0; i < 3; ++i) pin[i] = from_next(p[i]);
         if (k == j) {
           double Hd[15];
 #pragma unroll
@@ -416,13 +508,14 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       status = 3;
     }
 
+    STAMP(4);
     // ------------------------------------------------------------ forward sweep: dw, lambda+
     {
       double dxn[3] = {0, 0, 0};
       for (int j = 0; j <= N; ++j) {
         double dxi[3];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) dxi[i] = from<G>(dxn[i], k - 1);
+        for (int i = 0; i < 3; ++i) dxi[i] = from_prev(dxn[i]);
         if (k == j) {
           if (k == 0)
 #pragma unroll
@@ -453,6 +546,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       }
     }
 
+    STAMP(5);
     // ------------------------------------------------------------ bound-dual step, fraction to boundary
     double amax_l = 1.0, az_l = 1.0, tiny_l = 0.0, gd_l = 0.0;
 #pragma unroll
@@ -479,6 +573,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
     const double amax = gmin<G>(amax_l), az = gmin<G>(az_l), tiny = gmax<G>(tiny_l);
     const double gd = gsum<G>(gd_l);
 
+    STAMP(6);
     // ------------------------------------------------------------ filter line search
     double thk_l = 0, phk_l = hasU ? fs * qv : 0.0;
 #pragma unroll
@@ -504,7 +599,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       for (int i = 0; i < 5; ++i) zt[i] = z[i] + alpha * dz[i];
       double xtn[3];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) xtn[i] = from<G>(zt[i], k + 1);
+      for (int i = 0; i < 3; ++i) xtn[i] = from_next(zt[i]);
       double tht_l = 0, pht_l = 0;
       if (hasU) {
         double xft[3], qt;
@@ -552,6 +647,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       status = 3;
     }
 
+    STAMP(7);
     // ------------------------------------------------------------ update iterate
     if (!done) {
       if (!ftype) {  // augment the filter (entry slot fnext lives on lane fnext)
@@ -578,8 +674,16 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
         }
       }
     }
+    STAMP(8);
     sweep(true);
   }
+  STAMP(9);
+#ifdef MPCX_STAMPS
+  if (g_mpcx_stamps && (threadIdx.x & 63) == 0) {
+    const long wv = gid / 64;
+    for (int i = 0; i < 10; ++i) g_mpcx_stamps[wv * 10 + i] = st_acc[i];
+  }
+#endif
 
   // ---- results
   const double fsum = gsum<G>(hasU ? qv : 0.0);
@@ -689,6 +793,12 @@ __global__ void shift_kernel(int B, int N, int p_stride, int p_layout, StagePara
     }
   }
 }
+
+#ifdef MPCX_STAMPS
+extern "C" int mpcx_diag_set_stamp_buffer(void* d_buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_mpcx_stamps), &d_buf, sizeof(void*));
+}
+#endif
 
 // ---- launch helpers (called from capi.cpp) -----------------------------------
 hipError_t launch_solve(const SolveArgs& a, hipStream_t stream) {

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmpcx.so")
+LIB_PATH = os.environ.get("MPCX_LIB", os.path.join(_HERE, "libmpcx.so"))
 
 MODEL_UNICYCLE = 1
 COST_QUADRATURE = 0

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Per-phase cycle shares of the fused solve kernel (diagnostic build, -DMPCX_STAMPS).
+
+    make -C mpc-verde_amd stamps && python tools/stamp_profile.py [--steps S]
+
+Runs the bench workload (config 2 closed loop) on libmpcx_stamps.so; after the
+warm-up steps it records s_memtime deltas per solver phase for one solve and
+prints each phase's share and cycles per IPM iteration (slowest wave basis).
+Stamps perturb timing (they fence the scheduler); read shares, not totals.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["MPCX_LIB"] = os.path.join(ROOT, "mpc-verde_amd", "mpcx", "libmpcx_stamps.so")
+sys.path.insert(0, os.path.join(ROOT, "mpc-verde_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import mpcx  # noqa: E402
+from mpcx import dist  # noqa: E402
+from mpcx.device import DeviceLoop  # noqa: E402
+
+PHASES = ["errors", "barrier_update", "sigma", "riccati", "forward", "fraction", "linesearch", "update", "sweep",
+          "exit"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--N", type=int, default=20)
+    a = ap.parse_args()
+    lib = mpcx._lib.load()
+    lib.mpcx_diag_set_stamp_buffer.argtypes = [ctypes.c_void_p]
+    solver = mpcx.nlpsol("stamps", "mi355x", mpcx.unicycle_point_to_point(N=a.N))
+    loop = DeviceLoop(solver, dist.config2_inputs(0, a.batch))
+    for _ in range(a.steps):
+        loop.step()
+    G = 16 if a.N < 16 else (32 if a.N < 32 else 64)
+    waves = (a.batch * G + 63) // 64
+    buf = torch.zeros(waves * 10, dtype=torch.int64, device="cuda")
+    assert lib.mpcx_diag_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
+    loop.solve()
+    torch.cuda.synchronize()
+    acc = buf.view(waves, 10).cpu().numpy().astype(float)
+    iters = loop.iters.cpu().numpy().reshape(waves, -1).max(axis=1)
+    slow = int(np.argmax(acc.sum(axis=1)))
+    tot = acc[slow].sum()
+    out = {"iters_slowest_wave": int(iters[slow]), "cycles_slowest_wave": tot,
+           "cycles_per_iter": tot / max(iters[slow], 1),
+           "share": {p: round(acc[slow, i] / tot, 4) for i, p in enumerate(PHASES)},
+           "share_all_waves": {p: round(acc[:, i].sum() / acc.sum(), 4) for i, p in enumerate(PHASES)}}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
