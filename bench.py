@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--roofline-reps", type=int, default=20)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=4)
+    ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--profile-sweep-only", action="store_true", help="only launch the sweep (for rocprofv3 --pmc)")
     return ap.parse_args()
 
@@ -68,24 +68,46 @@ def shift_np(w, N):
     return w0
 
 
-def cpu_baseline(P0, N, steps, cores):
+def shift_lam_np(lam, N):
+    """Multipliers of g_k shifted like the states (the shift kernel's lam_g shift)."""
+    out = lam.copy()
+    out[:, :3 * N] = lam[:, 3:3 * (N + 1)]
+    return out
+
+
+def shift_lamx_np(lamx, N):
+    out = shift_np(lamx, N)
+    out[:, 0:3] = 0.0  # X_0 is free
+    return out
+
+
+def cpu_baseline(P0, N, steps, cores, warm=(1e-4, 1e-4, 1e-4)):
     """C++ oracle (port of the same NLP + IPOPT-style IPM) on host cores: `steps`
-    closed-loop steps of the same instances, solve calls timed."""
+    closed-loop steps of the same instances with the same warm start as the GPU
+    loop (first step cold, then shifted primal + multipliers), solve calls timed."""
     from oracle import ipm_ref, nlp_ref
 
     ipm_ref.build()
     ocp = nlp_ref.UnicycleOCP(N=N)
     P = P0.copy()
     B = P.shape[0]
-    w0 = None
+    w0 = _cold(P, N, nlp_ref)
+    lam0 = lamx0 = None
     t_solve = 0.0
-    for _ in range(steps):
+    for s in range(steps):
         t0 = time.perf_counter()
-        r = ipm_ref.solve_batch(ocp, P, w0=w0 if w0 is not None else _cold(P, N, nlp_ref), nthreads=cores)
+        if s == 0:
+            r = ipm_ref.solve_batch(ocp, P, w0=w0, nthreads=cores)
+            r["lam_x"] = np.zeros_like(r["w"])
+        else:
+            r = ipm_ref.solve_batch_warm(ocp, P, w0, lam0=lam0, lamx0=lamx0, mu_init=warm[0], bound_push=warm[1],
+                                         mult_push=warm[2], nthreads=cores)
         t_solve += time.perf_counter() - t0
         xf, _ = nlp_ref.F(P[:, 0:3], r["w"][:, 3:5], P[:, 3:6], ocp)
         P[:, 0:3] = xf
         w0 = shift_np(r["w"], N)
+        lam0 = shift_lam_np(r["lam_g"], N)
+        lamx0 = shift_lamx_np(r["lam_x"], N)
     return B * steps / t_solve, t_solve
 
 

@@ -89,6 +89,10 @@ typedef struct mpcx_spec {
   double R[8];          /* diagonal control weights (:81-84) */
   double lbu[8], ubu[8];/* control bounds (:42-45) */
   double lbx[8], ubx[8];/* state bounds (+-1e20 = free; Trajectory_tracking.py:64-67) */
+  /* Warm start (IPOPT warm_start_init_point = yes), used when multipliers are
+     passed in (lam_g0 / lam_x0 != NULL): initial barrier parameter, primal bound
+     push and bound-multiplier push.  Defaults 1e-4. */
+  double warm_mu_init, warm_bound_push, warm_mult_push;
 } mpcx_spec;
 
 /* Fill *s with the reference's constants for model/cost at horizon N
@@ -107,6 +111,10 @@ int mpcx_dims(const mpcx_handle* h, int32_t* n_w, int32_t* n_g, int32_t* n_p);
  *   P      B x n_p parameters (layout per spec.param_layout)
  *   w0     B x n_w initial guesses, or NULL = cold start (X_k = x0, U_k = 0,
  *          the reference's repmat(state_init) / zeros initialisation, :212-213)
+ *   lam_g0 B x n_g, lam_x0 B x n_w: initial multipliers (CasADi's lam_g0 /
+ *          lam_x0 solver inputs), or NULL.  If either is given the solve starts
+ *          as IPOPT's warm_start_init_point (spec.warm_*); otherwise as IPOPT's
+ *          default (mu = 0.1, multipliers 0 / 1).
  *   lbw/ubw n_w bound vectors shared by the batch, or NULL = spec bounds
  *          (the reference's lbx/ubx, :199-206; X_0 is always free: it is
  *          pinned by the lifted constraint g_0)
@@ -114,16 +122,19 @@ int mpcx_dims(const mpcx_handle* h, int32_t* n_w, int32_t* n_g, int32_t* n_p);
  *   f_out  B objective values, or NULL
  *   g_out  B x n_g constraint values at w_out, or NULL
  *   lam_g  B x n_g constraint multipliers (CasADi sign convention), or NULL
+ *   lam_x  B x n_w bound multipliers (CasADi convention: z_U - z_L), or NULL
  *   status B mpcx_status codes, or NULL
  *   iters  B iteration counts, or NULL                                        */
-int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w0, const double* lbw,
-                     const double* ubw, double* w_out, double* f_out, double* g_out, double* lam_g,
-                     int32_t* status, int32_t* iters);
+int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w0, const double* lam_g0,
+                     const double* lam_x0, const double* lbw, const double* ubw, double* w_out, double* f_out,
+                     double* g_out, double* lam_g, double* lam_x, int32_t* status, int32_t* iters);
 
 /* Device-pointer variant: no host synchronisation; all work is enqueued on
-   `stream` (a hipStream_t, NULL = default stream).  d_w0 may be NULL (cold). */
-int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const double* d_w0, double* d_w_out,
-                         double* d_f_out, double* d_lam_g, int32_t* d_status, int32_t* d_iters, void* stream);
+   `stream` (a hipStream_t, NULL = default stream).  Any d_* except d_P and
+   d_w_out may be NULL. */
+int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const double* d_w0, const double* d_lam_g0,
+                         const double* d_lam_x0, double* d_w_out, double* d_f_out, double* d_lam_g,
+                         double* d_lam_x, int32_t* d_status, int32_t* d_iters, void* stream);
 
 /* Plant / integrator F (host): xf = F(x0, u).xf, qf = F(x0, u).qf for B
    instances; P as in mpcx_solve_batch (only x0 and the stage-0 reference are
@@ -132,8 +143,12 @@ int mpcx_plant_step(mpcx_handle* h, int32_t B, const double* P, const double* u,
 
 /* Receding-horizon update on the device (one closed-loop step of
    Casadi/multiple_shooting_casadi.py:271-287): x0 <- F(x0, u_0*) in d_P, and
-   d_w0_next = the optimal w shifted by one interval (last interval repeated). */
-int mpcx_shift_dev(mpcx_handle* h, int32_t B, double* d_P, const double* d_w, double* d_w0_next, void* stream);
+   d_w0_next = the optimal w shifted by one interval (last interval repeated).
+   If d_lam_g / d_lam_x are given, the multipliers are shifted the same way into
+   d_lam_g0_next / d_lam_x0_next (warm start of the next solve). */
+int mpcx_shift_dev(mpcx_handle* h, int32_t B, double* d_P, const double* d_w, double* d_w0_next,
+                   const double* d_lam_g, double* d_lam_g0_next, const double* d_lam_x, double* d_lam_x0_next,
+                   void* stream);
 
 /* RK4 + Jacobian sweep over B x N shooting intervals (host pointers).
  *   w      B x n_w decision vectors (interleaved layout)

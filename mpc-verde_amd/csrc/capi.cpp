@@ -26,6 +26,7 @@ struct mpcx_handle {
   // workspace (grown on demand)
   size_t cap_B = 0;
   double *d_P = nullptr, *d_w0 = nullptr, *d_w = nullptr, *d_f = nullptr, *d_lam = nullptr;
+  double *d_lam0 = nullptr, *d_lamx0 = nullptr, *d_lamx = nullptr;
   int32_t *d_status = nullptr, *d_iters = nullptr;
   size_t cap_sweep = 0;
   double* d_sweep = nullptr;
@@ -85,6 +86,9 @@ int ensure(mpcx_handle* h, size_t B) {
   (void)hipFree(h->d_lam);
   (void)hipFree(h->d_status);
   (void)hipFree(h->d_iters);
+  (void)hipFree(h->d_lam0);
+  (void)hipFree(h->d_lamx0);
+  (void)hipFree(h->d_lamx);
   h->cap_B = 0;
   HIPCHK(hipMalloc(&h->d_P, nb * h->np * sizeof(double)));
   HIPCHK(hipMalloc(&h->d_w0, nb * h->nw * sizeof(double)));
@@ -93,6 +97,9 @@ int ensure(mpcx_handle* h, size_t B) {
   HIPCHK(hipMalloc(&h->d_lam, nb * h->ng * sizeof(double)));
   HIPCHK(hipMalloc(&h->d_status, nb * sizeof(int32_t)));
   HIPCHK(hipMalloc(&h->d_iters, nb * sizeof(int32_t)));
+  HIPCHK(hipMalloc(&h->d_lam0, nb * h->ng * sizeof(double)));
+  HIPCHK(hipMalloc(&h->d_lamx0, nb * h->nw * sizeof(double)));
+  HIPCHK(hipMalloc(&h->d_lamx, nb * h->nw * sizeof(double)));
   h->cap_B = nb;
   return 0;
 }
@@ -134,6 +141,9 @@ int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N) {
     s->lbx[i] = -1e20;
     s->ubx[i] = 1e20;
   }
+  s->warm_mu_init = 1e-4;
+  s->warm_bound_push = 1e-4;
+  s->warm_mult_push = 1e-4;
   return 0;
 }
 
@@ -148,6 +158,8 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
     return fail(MPCX_EINVAL, "unknown param_layout");
   if (s->max_iter < 0) return fail(MPCX_EINVAL, "max_iter < 0");
   if (!(s->tol > 0)) return fail(MPCX_EINVAL, "tol must be > 0");
+  if (!(s->warm_mu_init > 0) || !(s->warm_bound_push > 0) || !(s->warm_mult_push > 0))
+    return fail(MPCX_EINVAL, "warm_mu_init / warm_bound_push / warm_mult_push must be > 0");
   for (int i = 0; i < 2; ++i)
     if (!(s->lbu[i] < s->ubu[i])) return fail(MPCX_EINVAL, "lbu must be < ubu");
   for (int i = 0; i < 3; ++i)
@@ -193,6 +205,9 @@ void mpcx_destroy(mpcx_handle* h) {
   (void)hipFree(h->d_lam);
   (void)hipFree(h->d_status);
   (void)hipFree(h->d_iters);
+  (void)hipFree(h->d_lam0);
+  (void)hipFree(h->d_lamx0);
+  (void)hipFree(h->d_lamx);
   (void)hipFree(h->d_sweep);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -206,8 +221,9 @@ int mpcx_dims(const mpcx_handle* h, int32_t* n_w, int32_t* n_g, int32_t* n_p) {
   return 0;
 }
 
-static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, const double* w0, const double* lbw,
-                                 const double* ubw, double* w, double* f, double* lam, int32_t* st, int32_t* it) {
+static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, const double* w0, const double* lam0,
+                                 const double* lamx0, const double* lbw, const double* ubw, double* w, double* f,
+                                 double* lam, double* lamx, int32_t* st, int32_t* it) {
   mpcx::SolveArgs a;
   a.B = B;
   a.N = h->spec.N;
@@ -218,30 +234,39 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
   a.sp = stage_params(h->spec);
   a.P = P;
   a.w0 = w0;
+  a.lam0 = lam0;
+  a.lamx0 = lamx0;
+  a.warm = (lam0 || lamx0) ? 1 : 0;
+  a.mu_init = h->spec.warm_mu_init;
+  a.bound_push = h->spec.warm_bound_push;
+  a.mult_push = h->spec.warm_mult_push;
   a.lbw = lbw;
   a.ubw = ubw;
   a.w_out = w;
   a.f_out = f;
   a.lam_out = lam;
+  a.lamx_out = lamx;
   a.status = st;
   a.iters = it;
   return a;
 }
 
-int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const double* d_w0, double* d_w_out,
-                         double* d_f_out, double* d_lam_g, int32_t* d_status, int32_t* d_iters, void* stream) {
+int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const double* d_w0, const double* d_lam_g0,
+                         const double* d_lam_x0, double* d_w_out, double* d_f_out, double* d_lam_g,
+                         double* d_lam_x, int32_t* d_status, int32_t* d_iters, void* stream) {
   if (!h || !d_P || !d_w_out) return fail(MPCX_EINVAL, "null argument");
   if (B < 0) return fail(MPCX_EINVAL, "B < 0");
   if (B == 0) return 0;
   HIPCHK(hipSetDevice(h->spec.device));
-  mpcx::SolveArgs a = make_args(h, B, d_P, d_w0, h->d_lbw, h->d_ubw, d_w_out, d_f_out, d_lam_g, d_status, d_iters);
+  mpcx::SolveArgs a = make_args(h, B, d_P, d_w0, d_lam_g0, d_lam_x0, h->d_lbw, h->d_ubw, d_w_out, d_f_out, d_lam_g,
+                                d_lam_x, d_status, d_iters);
   HIPCHK(mpcx::launch_solve(a, (hipStream_t)stream));
   return 0;
 }
 
-int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w0, const double* lbw,
-                     const double* ubw, double* w_out, double* f_out, double* g_out, double* lam_g, int32_t* status,
-                     int32_t* iters) {
+int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w0, const double* lam_g0,
+                     const double* lam_x0, const double* lbw, const double* ubw, double* w_out, double* f_out,
+                     double* g_out, double* lam_g, double* lam_x, int32_t* status, int32_t* iters) {
   if (!h || !P || !w_out) return fail(MPCX_EINVAL, "null argument");
   if (B < 0) return fail(MPCX_EINVAL, "B < 0");
   if (B == 0) return 0;
@@ -272,9 +297,13 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
   }
   HIPCHK(hipMemcpyAsync(h->d_P, P, (size_t)B * h->np * sizeof(double), hipMemcpyHostToDevice, s));
   if (w0) HIPCHK(hipMemcpyAsync(h->d_w0, w0, (size_t)B * h->nw * sizeof(double), hipMemcpyHostToDevice, s));
-  mpcx::SolveArgs a = make_args(h, B, h->d_P, w0 ? h->d_w0 : nullptr, dl, du, h->d_w, h->d_f,
-                                (lam_g ? h->d_lam : nullptr), h->d_status, h->d_iters);
+  if (lam_g0) HIPCHK(hipMemcpyAsync(h->d_lam0, lam_g0, (size_t)B * h->ng * sizeof(double), hipMemcpyHostToDevice, s));
+  if (lam_x0) HIPCHK(hipMemcpyAsync(h->d_lamx0, lam_x0, (size_t)B * h->nw * sizeof(double), hipMemcpyHostToDevice, s));
+  mpcx::SolveArgs a = make_args(h, B, h->d_P, w0 ? h->d_w0 : nullptr, lam_g0 ? h->d_lam0 : nullptr,
+                                lam_x0 ? h->d_lamx0 : nullptr, dl, du, h->d_w, h->d_f, (lam_g ? h->d_lam : nullptr),
+                                (lam_x ? h->d_lamx : nullptr), h->d_status, h->d_iters);
   HIPCHK(mpcx::launch_solve(a, s));
+  if (lam_x) HIPCHK(hipMemcpyAsync(lam_x, h->d_lamx, (size_t)B * h->nw * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(w_out, h->d_w, (size_t)B * h->nw * sizeof(double), hipMemcpyDeviceToHost, s));
   if (f_out) HIPCHK(hipMemcpyAsync(f_out, h->d_f, (size_t)B * sizeof(double), hipMemcpyDeviceToHost, s));
   if (lam_g) HIPCHK(hipMemcpyAsync(lam_g, h->d_lam, (size_t)B * h->ng * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -331,12 +360,16 @@ int mpcx_plant_step(mpcx_handle* h, int32_t B, const double* P, const double* u,
   return 0;
 }
 
-int mpcx_shift_dev(mpcx_handle* h, int32_t B, double* d_P, const double* d_w, double* d_w0_next, void* stream) {
+int mpcx_shift_dev(mpcx_handle* h, int32_t B, double* d_P, const double* d_w, double* d_w0_next,
+                   const double* d_lam_g, double* d_lam_g0_next, const double* d_lam_x, double* d_lam_x0_next,
+                   void* stream) {
   if (!h || !d_P || !d_w || !d_w0_next) return fail(MPCX_EINVAL, "null argument");
   if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
+  if ((d_lam_g == nullptr) != (d_lam_g0_next == nullptr) || (d_lam_x == nullptr) != (d_lam_x0_next == nullptr))
+    return fail(MPCX_EINVAL, "multiplier shift needs both source and destination");
   HIPCHK(hipSetDevice(h->spec.device));
   HIPCHK(mpcx::launch_shift(B, h->spec.N, h->np, h->spec.param_layout, stage_params(h->spec), d_P, d_w, d_w0_next,
-                            (hipStream_t)stream));
+                            d_lam_g, d_lam_g0_next, d_lam_x, d_lam_x0_next, (hipStream_t)stream));
   return 0;
 }
 

@@ -278,22 +278,35 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       for (int i = 0; i < 3; ++i) z[i] = x0[i];  // repmat(state_init), U = 0
     }
   }
+  // bound push (IPOPT bound_push / bound_frac = 1e-2; warm start: warm_start_bound_push)
+  const bool warm = a.warm != 0;
+  const double push = warm ? a.bound_push : kBoundPush, frac = warm ? a.bound_push : kBoundFrac;
+  double lx0[5] = {0, 0, 0, 0, 0};  // given bound multipliers (zU - zL) of my variables
+  if (warm && a.lamx0 && hasX) {
+    const double* l = a.lamx0 + (size_t)inst * nw;
+    if (k > 0)
+      for (int i = 0; i < 3; ++i) lx0[i] = l[ixw(k, i)];
+    if (hasU)
+      for (int i = 0; i < 2; ++i) lx0[3 + i] = l[iuw(k, i)];
+  }
   double zL[5], zU[5];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {  // bound push (IPOPT bound_push / bound_frac = 1e-2)
+  for (int i = 0; i < 5; ++i) {
     if (hL[i] && hU[i]) {
-      const double pl = fmin(kBoundPush * fmax(1.0, fabs(lb[i])), kBoundFrac * (ub[i] - lb[i]));
-      const double pu = fmin(kBoundPush * fmax(1.0, fabs(ub[i])), kBoundFrac * (ub[i] - lb[i]));
+      const double pl = fmin(push * fmax(1.0, fabs(lb[i])), frac * (ub[i] - lb[i]));
+      const double pu = fmin(push * fmax(1.0, fabs(ub[i])), frac * (ub[i] - lb[i]));
       z[i] = fmin(fmax(z[i], lb[i] + pl), ub[i] - pu);
     } else if (hL[i]) {
-      z[i] = fmax(z[i], lb[i] + kBoundPush * fmax(1.0, fabs(lb[i])));
+      z[i] = fmax(z[i], lb[i] + push * fmax(1.0, fabs(lb[i])));
     } else if (hU[i]) {
-      z[i] = fmin(z[i], ub[i] - kBoundPush * fmax(1.0, fabs(ub[i])));
+      z[i] = fmin(z[i], ub[i] - push * fmax(1.0, fabs(ub[i])));
     }
-    zL[i] = hL[i] ? 1.0 : 0.0;
-    zU[i] = hU[i] ? 1.0 : 0.0;
+    zL[i] = hL[i] ? (warm ? fmax(-lx0[i], a.mult_push) : 1.0) : 0.0;
+    zU[i] = hU[i] ? (warm ? fmax(lx0[i], a.mult_push) : 1.0) : 0.0;
   }
   double lam[3] = {0, 0, 0};  // lambda_k: multiplier of g_k (defines X_k)
+  if (warm && a.lam0 && hasX)
+    for (int i = 0; i < 3; ++i) lam[i] = a.lam0[(size_t)inst * ng + 3 * k + i];
 
   // ---- stage evaluation helpers (all lanes execute; hasU masks)
   double xf[3], qv, A[9], Bm[6], gq[5], Hs[15];
@@ -333,10 +346,20 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
     for (int i = 0; i < 5; ++i) gm = fmax(gm, fabs(gq[i]));
     gm = gmax<G>(gm);
     fs = gm > 100.0 ? 100.0 / gm : 1.0;
-    if (fs != 1.0) sweep(true);  // group-uniform
+    if (fs != 1.0) {  // group-uniform; given multipliers belong to the unscaled problem
+#pragma unroll
+      for (int i = 0; i < 3; ++i) lam[i] *= fs;
+      if (warm)
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          if (hL[i]) zL[i] = fmax(zL[i] * fs, a.mult_push);
+          if (hU[i]) zU[i] = fmax(zU[i] * fs, a.mult_push);
+        }
+      sweep(true);
+    }
   }
 
-  double mu = 0.1, tau = fmax(kTauMin, 1.0 - mu);
+  double mu = warm ? a.mu_init : 0.1, tau = fmax(kTauMin, 1.0 - mu);
   const double mu_min = a.tol / 10.0;
   double theta0 = 0;
 #pragma unroll
@@ -695,6 +718,13 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       for (int i = 0; i < 2; ++i) w[iuw(k, i)] = z[3 + i];
     if (a.lam_out && hasX)
       for (int i = 0; i < 3; ++i) a.lam_out[(size_t)inst * ng + 3 * k + i] = lam[i] / fs;
+    if (a.lamx_out) {
+      double* lx = a.lamx_out + (size_t)inst * nw;
+      if (hasX)
+        for (int i = 0; i < 3; ++i) lx[ixw(k, i)] = (zU[i] - zL[i]) / fs;
+      if (hasU)
+        for (int i = 0; i < 2; ++i) lx[iuw(k, i)] = (zU[3 + i] - zL[3 + i]) / fs;
+    }
     if (k == 0) {
       if (a.f_out) a.f_out[inst] = fsum;
       if (a.status) a.status[inst] = status;
@@ -766,12 +796,14 @@ __global__ void plant_kernel(int B, int p_stride, int p_layout, StageParams sp, 
   if (QF) QF[b] = q;
 }
 
-// Closed-loop update (:271-287): x0 <- F(x0, u0*), w0_next = w shifted one interval.
+// Closed-loop update (:271-287): x0 <- F(x0, u0*), w0_next = w shifted one interval;
+// multipliers shifted alike when given (warm start of the next solve).
 __global__ void shift_kernel(int B, int N, int p_stride, int p_layout, StageParams sp, double* __restrict__ P,
-                             const double* __restrict__ W, double* __restrict__ W0) {
+                             const double* __restrict__ W, double* __restrict__ W0, const double* __restrict__ L,
+                             double* __restrict__ L0, const double* __restrict__ LX, double* __restrict__ LX0) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  const int nw = 3 + 5 * N;
+  const int nw = 3 + 5 * N, ng = 3 * (N + 1);
   double* p = P + (size_t)b * p_stride;
   const double* w = W + (size_t)b * nw;
   double* w0 = W0 + (size_t)b * nw;
@@ -787,9 +819,15 @@ __global__ void shift_kernel(int B, int N, int p_stride, int p_layout, StagePara
   for (int kk = 0; kk <= N; ++kk) {
     const int src = kk < N ? kk + 1 : N;
     for (int i = 0; i < 3; ++i) w0[ixw(kk, i)] = w[ixw(src, i)];
+    if (LX && LX0)
+      for (int i = 0; i < 3; ++i) LX0[(size_t)b * nw + ixw(kk, i)] = kk == 0 ? 0.0 : LX[(size_t)b * nw + ixw(src, i)];
+    if (L && L0)
+      for (int i = 0; i < 3; ++i) L0[(size_t)b * ng + 3 * kk + i] = L[(size_t)b * ng + 3 * src + i];
     if (kk < N) {
       const int su = kk + 1 < N ? kk + 1 : N - 1;
       for (int i = 0; i < 2; ++i) w0[iuw(kk, i)] = w[iuw(su, i)];
+      if (LX && LX0)
+        for (int i = 0; i < 2; ++i) LX0[(size_t)b * nw + iuw(kk, i)] = LX[(size_t)b * nw + iuw(su, i)];
     }
   }
 }
@@ -827,8 +865,9 @@ hipError_t launch_plant(int B, int p_stride, int p_layout, const StageParams& sp
 }
 
 hipError_t launch_shift(int B, int N, int p_stride, int p_layout, const StageParams& sp, double* P, const double* W,
-                        double* W0, hipStream_t stream) {
-  hipLaunchKernelGGL(shift_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, B, N, p_stride, p_layout, sp, P, W, W0);
+                        double* W0, const double* L, double* L0, const double* LX, double* LX0, hipStream_t stream) {
+  hipLaunchKernelGGL(shift_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, B, N, p_stride, p_layout, sp, P, W, W0,
+                     L, L0, LX, LX0);
   return hipGetLastError();
 }
 

@@ -35,7 +35,8 @@ class Spec(ctypes.Structure):
                 ("device", ctypes.c_int32), ("reserved", ctypes.c_int32), ("T", ctypes.c_double),
                 ("tol", ctypes.c_double), ("Q", ctypes.c_double * 8), ("R", ctypes.c_double * 8),
                 ("lbu", ctypes.c_double * 8), ("ubu", ctypes.c_double * 8), ("lbx", ctypes.c_double * 8),
-                ("ubx", ctypes.c_double * 8)]
+                ("ubx", ctypes.c_double * 8), ("warm_mu_init", ctypes.c_double),
+                ("warm_bound_push", ctypes.c_double), ("warm_mult_push", ctypes.c_double)]
 
 
 _lib = None
@@ -45,6 +46,29 @@ class MpcxError(RuntimeError):
     pass
 
 
+def _bind_single_hip_runtime():
+    """Make libmpcx resolve libamdhip64.so.7 to the copy PyTorch uses, if PyTorch is installed.
+
+    PyTorch-ROCm ships its own libamdhip64 (NEEDED as "libamdhip64.so", found via
+    its RPATH) while libmpcx is linked against /opt/rocm's (NEEDED
+    "libamdhip64.so.7"); both carry the soname libamdhip64.so.7.  Loaded in the
+    wrong order a process ends up with two HIP runtimes, and the second one cannot
+    open the GPU ("No HIP GPUs are available").  Loading PyTorch's copy first
+    (without importing torch) makes every later lookup resolve to that one file.
+    """
+    import importlib.util
+
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.origin:
+        return
+    p = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(p):
+        ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+
+
 def load():
     """Load libmpcx.so (raises if it has not been built)."""
     global _lib
@@ -52,6 +76,7 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise MpcxError(f"{LIB_PATH} not found: build it with `make -C mpc-verde_amd` (hipcc, gfx950)")
+    _bind_single_hip_runtime()
     lib = ctypes.CDLL(LIB_PATH)
     dp = ctypes.POINTER(ctypes.c_double)
     ip = ctypes.POINTER(ctypes.c_int32)
@@ -63,10 +88,10 @@ def load():
     lib.mpcx_destroy.restype = None
     lib.mpcx_last_error.restype = ctypes.c_char_p
     lib.mpcx_dims.argtypes = [H, ip, ip, ip]
-    lib.mpcx_solve_batch.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp, dp, dp, dp, dp, ip, ip]
-    lib.mpcx_solve_batch_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.mpcx_solve_batch.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, ip, ip]
+    lib.mpcx_solve_batch_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mpcx_plant_step.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp]
-    lib.mpcx_shift_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp]
+    lib.mpcx_shift_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mpcx_rk4_sens.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp, dp, dp, dp]
     lib.mpcx_rk4_sens_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     for name in EXPORTS:

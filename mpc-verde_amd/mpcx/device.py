@@ -29,23 +29,29 @@ class DeviceLoop:
     """B independent MPC instances stepped on one GPU.
 
     P (B, n_p) float64 parameters live on the device; w holds the last solution
-    and w0 the shifted warm start.  ``step()`` enqueues a solve and the plant
-    update on ``stream`` and returns immediately.
+    and w0 the shifted warm start.  With warm_duals (default) the constraint and
+    bound multipliers are shifted as well and the next solve starts as IPOPT's
+    warm_start_init_point (spec.warm_*); the first solve is always cold.
+    ``step()`` enqueues a solve and the plant/shift update on ``stream`` and
+    returns immediately.
     """
 
-    def __init__(self, solver: Solver, P0, device="cuda", stream=None, cold_first=True):
+    def __init__(self, solver: Solver, P0, device="cuda", stream=None, cold_first=True, warm_duals=True):
         self.solver = solver
         self.device = torch.device(device)
         P0 = np.ascontiguousarray(np.asarray(P0, np.float64))
         self.B = P0.shape[0]
         nw, ng = solver._h.n_w, solver._h.n_g
+        z = lambda *s: torch.zeros(s, dtype=torch.float64, device=self.device)  # noqa: E731
         self.P = torch.from_numpy(P0).to(self.device)
-        self.w = torch.zeros((self.B, nw), dtype=torch.float64, device=self.device)
-        self.w0 = torch.zeros((self.B, nw), dtype=torch.float64, device=self.device)
-        self.f = torch.zeros(self.B, dtype=torch.float64, device=self.device)
+        self.w, self.w0 = z(self.B, nw), z(self.B, nw)
+        self.lam, self.lam0 = z(self.B, ng), z(self.B, ng)
+        self.lamx, self.lamx0 = z(self.B, nw), z(self.B, nw)
+        self.f = z(self.B)
         self.status = torch.zeros(self.B, dtype=torch.int32, device=self.device)
         self.iters = torch.zeros(self.B, dtype=torch.int32, device=self.device)
         self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.warm_duals = warm_duals
         self._cold = cold_first
 
     def solve(self, status_out=None, iters_out=None):
@@ -55,16 +61,22 @@ class DeviceLoop:
         lib = _lib.load()
         s = ctypes_void(self.stream.cuda_stream)
         w0 = None if self._cold else _ptr(self.w0)
+        warm = self.warm_duals and not self._cold
         st = self.status if status_out is None else status_out
         it = self.iters if iters_out is None else iters_out
-        _lib.check(lib.mpcx_solve_batch_dev(self.solver._h.ptr, self.B, _ptr(self.P), w0, _ptr(self.w),
-                                            _ptr(self.f), None, _ptr(st), _ptr(it), s))
+        _lib.check(lib.mpcx_solve_batch_dev(self.solver._h.ptr, self.B, _ptr(self.P), w0,
+                                            _ptr(self.lam0) if warm else None, _ptr(self.lamx0) if warm else None,
+                                            _ptr(self.w), _ptr(self.f), _ptr(self.lam), _ptr(self.lamx), _ptr(st),
+                                            _ptr(it), s))
         self._cold = False
 
     def shift(self):
         lib = _lib.load()
         s = ctypes_void(self.stream.cuda_stream)
-        _lib.check(lib.mpcx_shift_dev(self.solver._h.ptr, self.B, _ptr(self.P), _ptr(self.w), _ptr(self.w0), s))
+        d = self.warm_duals
+        _lib.check(lib.mpcx_shift_dev(self.solver._h.ptr, self.B, _ptr(self.P), _ptr(self.w), _ptr(self.w0),
+                                      _ptr(self.lam) if d else None, _ptr(self.lam0) if d else None,
+                                      _ptr(self.lamx) if d else None, _ptr(self.lamx0) if d else None, s))
 
     def step(self):
         self.solve()

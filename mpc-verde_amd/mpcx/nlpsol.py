@@ -79,11 +79,14 @@ class Solver:
         return dict(self._stats)
 
     # ---------------------------------------------------------------- batched core
-    def solve_batch(self, P, w0=None, lbw=None, ubw=None, want_lam=True, want_g=False):
+    def solve_batch(self, P, w0=None, lbw=None, ubw=None, want_lam=True, want_g=False, lam_g0=None, lam_x0=None):
         """Solve B independent NLPs (multiple-shooting layout).
 
-        P (B, n_p); w0 (B, n_w) or None (cold start X_k = x0, U = 0).
-        Returns dict of arrays: w (B,n_w), f (B,), lam_g (B,n_g), status (B,), iters (B,), g (B,n_g).
+        P (B, n_p); w0 (B, n_w) or None (cold start X_k = x0, U = 0);
+        lam_g0 (B, n_g) / lam_x0 (B, n_w): warm-start multipliers (IPOPT
+        warm_start_init_point), or None.
+        Returns dict of arrays: w (B,n_w), f (B,), lam_g (B,n_g), lam_x (B,n_w), status (B,), iters (B,),
+        g (B,n_g).
         """
         P = np.ascontiguousarray(np.atleast_2d(np.asarray(P, np.float64)))
         B = P.shape[0]
@@ -93,19 +96,22 @@ class Solver:
         w0a = None
         if w0 is not None:
             w0a = np.ascontiguousarray(np.asarray(w0, np.float64).reshape(B, nw))
+        l0 = None if lam_g0 is None else np.ascontiguousarray(np.asarray(lam_g0, np.float64).reshape(B, ng))
+        lx0 = None if lam_x0 is None else np.ascontiguousarray(np.asarray(lam_x0, np.float64).reshape(B, nw))
         w = np.empty((B, nw))
         f = np.empty(B)
         lam = np.empty((B, ng)) if want_lam else None
+        lamx = np.empty((B, nw)) if want_lam else None
         g = np.empty((B, ng)) if want_g else None
         st = np.empty(B, np.int32)
         it = np.empty(B, np.int32)
         lib = _lib.load()
         t0 = time.perf_counter()
-        _lib.check(lib.mpcx_solve_batch(self._h.ptr, B, _lib.dptr(P), _lib.dptr(w0a), _lib.dptr(lbw), _lib.dptr(ubw),
-                                        _lib.dptr(w), _lib.dptr(f), _lib.dptr(g), _lib.dptr(lam), _lib.iptr(st),
-                                        _lib.iptr(it)))
+        _lib.check(lib.mpcx_solve_batch(self._h.ptr, B, _lib.dptr(P), _lib.dptr(w0a), _lib.dptr(l0), _lib.dptr(lx0),
+                                        _lib.dptr(lbw), _lib.dptr(ubw), _lib.dptr(w), _lib.dptr(f), _lib.dptr(g),
+                                        _lib.dptr(lam), _lib.dptr(lamx), _lib.iptr(st), _lib.iptr(it)))
         t = time.perf_counter() - t0
-        return {"w": w, "f": f, "lam_g": lam, "g": g, "status": st, "iters": it, "t_wall": t}
+        return {"w": w, "f": f, "lam_g": lam, "lam_x": lamx, "g": g, "status": st, "iters": it, "t_wall": t}
 
     def rk4_sens(self, w, P):
         """Per-interval defects, costs and Jacobians at w (B, n_w) -- the sweep kernel."""
@@ -121,8 +127,9 @@ class Solver:
                                              _lib.dptr(A), _lib.dptr(Bm), _lib.dptr(gq)))
         return {"c": c, "q": q, "A": A, "B": Bm, "gq": gq}
 
-    def lam_x(self, w, P, lam_g):
-        """Bound multipliers in CasADi's convention: grad f + J^T lam_g + lam_x = 0."""
+    def lam_x_from_kkt(self, w, P, lam_g):
+        """Bound multipliers reconstructed from stationarity, grad f + J^T lam_g + lam_x = 0
+        (evaluated with the sweep kernel; used to cross-check the solver's own lam_x)."""
         s = self.rk4_sens(w, P)
         B, N = s["q"].shape
         r = np.zeros((B, self._h.n_w))
@@ -153,6 +160,7 @@ class Solver:
         elif np.any(lbg != 0) or np.any(ubg != 0):
             raise ValueError("multiple shooting: g are the shooting equalities, lbg = ubg = 0 required")
         N = ocp.N
+        l0 = lx0 = None
         if ss:  # decision = U; bounds on U map onto the U slots of the multiple-shooting w
             lbw = np.full(self._h.n_w, -1e20)
             ubw = np.full(self._h.n_w, 1e20)
@@ -167,15 +175,17 @@ class Solver:
         else:
             lbw, ubw = lbx, ubx
             w0 = None if x0 is None else _vec(x0, self._h.n_w, "x0")[None, :]
+            l0 = None if lam_g0 is None else _vec(lam_g0, self._h.n_g, "lam_g0")[None, :]
+            lx0 = None if lam_x0 is None else _vec(lam_x0, self._h.n_w, "lam_x0")[None, :]
         lbw = np.where(np.isfinite(lbw), lbw, -1e20)
         ubw = np.where(np.isfinite(ubw), ubw, 1e20)
         r = self.solve_batch(P, w0, np.ascontiguousarray(lbw), np.ascontiguousarray(ubw), want_lam=True,
-                             want_g=True)
+                             want_g=True, lam_g0=l0, lam_x0=lx0)
         st = int(r["status"][0])
         self._stats = {"return_status": _lib.STATUS.get(st, str(st)), "success": st <= 1,
                        "iter_count": int(r["iters"][0]), "t_wall_total": r["t_wall"], "status_code": st}
         w = r["w"][0]
-        lam_x = self.lam_x(r["w"], P, r["lam_g"])[0]
+        lam_x = r["lam_x"][0]
         if ss:
             U = np.stack([w[3 + 5 * k:5 + 5 * k] for k in range(N)]).reshape(-1)
             Xs = np.stack([w[5 + 5 * k:8 + 5 * k] for k in range(N)])

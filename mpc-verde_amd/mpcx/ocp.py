@@ -76,7 +76,7 @@ def unicycle_tracking(N=10, T=0.2):
                x_ub=(20.0, 2.0, math.inf), cost="node", param="x0_stageref")
 
 
-def to_spec(ocp: OCP, max_iter=2000, tol=1e-8, device=0) -> _lib.Spec:
+def to_spec(ocp: OCP, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4)) -> _lib.Spec:
     if ocp.model != "unicycle":
         raise ValueError(f"unsupported model {ocp.model!r}")
     s = _lib.Spec()
@@ -85,6 +85,7 @@ def to_spec(ocp: OCP, max_iter=2000, tol=1e-8, device=0) -> _lib.Spec:
     s.param_layout = {"x0_xref": _lib.P_X0_XREF, "x0_stageref": _lib.P_X0_STAGEREF}[ocp.param]
     s.N, s.M, s.max_iter, s.device = int(ocp.N), int(ocp.M), int(max_iter), int(device)
     s.T, s.tol = float(ocp.T), float(tol)
+    s.warm_mu_init, s.warm_bound_push, s.warm_mult_push = (float(v) for v in warm)
     big = 1e20
 
     def fin(v, default):

@@ -406,27 +406,38 @@ double norm1(const std::vector<double>& v) {
 }
 
 // Solve one instance.  Returns status: 0 converged, 1 acceptable, 2 max_iter, 3 failure
-int solve_one(Instance& I, double* w, double* lam, int max_iter, double tol, int* iters_out, double* f_out) {
+// Warm-start options (IPOPT warm_start_init_point = yes): multipliers from a previous
+// solve, smaller initial barrier and bound pushes.  warm == nullptr -> IPOPT defaults.
+struct Warm {
+  double mu_init, bound_push, mult_push;
+  const double* lam0;   // ng
+  const double* lamx0;  // nw, CasADi convention lam_x = zU - zL
+};
+
+int solve_one(Instance& I, double* w, double* lam, int max_iter, double tol, int* iters_out, double* f_out,
+              const Warm* warm = nullptr, double* lamx_out = nullptr) {
   const int N = I.N, nw = I.nw, ng = 3 * (N + 1);
+  const double push = warm ? warm->bound_push : kBoundPush;
   // ---- initial point: bound push (IPOPT bound_push / bound_frac)
   for (int i = 0; i < nw; ++i) {
     if (I.hasL[i] && I.hasU[i]) {
-      double pl = std::min(kBoundPush * std::max(1.0, std::fabs(I.lb[i])), kBoundFrac * (I.ub[i] - I.lb[i]));
-      double pu = std::min(kBoundPush * std::max(1.0, std::fabs(I.ub[i])), kBoundFrac * (I.ub[i] - I.lb[i]));
+      double pl = std::min(push * std::max(1.0, std::fabs(I.lb[i])), push * (I.ub[i] - I.lb[i]));
+      double pu = std::min(push * std::max(1.0, std::fabs(I.ub[i])), push * (I.ub[i] - I.lb[i]));
       w[i] = std::min(std::max(w[i], I.lb[i] + pl), I.ub[i] - pu);
     } else if (I.hasL[i]) {
-      w[i] = std::max(w[i], I.lb[i] + kBoundPush * std::max(1.0, std::fabs(I.lb[i])));
+      w[i] = std::max(w[i], I.lb[i] + push * std::max(1.0, std::fabs(I.lb[i])));
     } else if (I.hasU[i]) {
-      w[i] = std::min(w[i], I.ub[i] - kBoundPush * std::max(1.0, std::fabs(I.ub[i])));
+      w[i] = std::min(w[i], I.ub[i] - push * std::max(1.0, std::fabs(I.ub[i])));
     }
   }
   std::vector<double> zL(nw, 0.0), zU(nw, 0.0);
   int nbound = 0;
   for (int i = 0; i < nw; ++i) {
-    if (I.hasL[i]) { zL[i] = 1.0; ++nbound; }
-    if (I.hasU[i]) { zU[i] = 1.0; ++nbound; }
+    const double lx = (warm && warm->lamx0) ? warm->lamx0[i] : 0.0;
+    if (I.hasL[i]) { zL[i] = warm ? std::max(-lx, warm->mult_push) : 1.0; ++nbound; }
+    if (I.hasU[i]) { zU[i] = warm ? std::max(lx, warm->mult_push) : 1.0; ++nbound; }
   }
-  for (int i = 0; i < ng; ++i) lam[i] = 0.0;
+  for (int i = 0; i < ng; ++i) lam[i] = (warm && warm->lam0) ? warm->lam0[i] : 0.0;
   // ---- gradient-based objective scaling (IPOPT nlp_scaling_max_gradient = 100)
   Eval e;
   I.fscale = 1.0;
@@ -436,10 +447,16 @@ int solve_one(Instance& I, double* w, double* lam, int max_iter, double tol, int
     for (double g : e.grad) gmax = std::max(gmax, std::fabs(g));
     if (gmax > 100.0) {
       I.fscale = 100.0 / gmax;
+      // multipliers given for the unscaled problem scale with the objective
+      for (int i = 0; i < ng; ++i) lam[i] *= I.fscale;
+      for (int i = 0; i < nw; ++i) {
+        if (warm && I.hasL[i]) zL[i] = std::max(zL[i] * I.fscale, warm->mult_push);
+        if (warm && I.hasU[i]) zU[i] = std::max(zU[i] * I.fscale, warm->mult_push);
+      }
       evaluate(I, w, lam, true, e);
     }
   }
-  double mu = 0.1, tau = std::max(kTauMin, 1.0 - mu);
+  double mu = warm ? warm->mu_init : 0.1, tau = std::max(kTauMin, 1.0 - mu);
   const double mu_min = tol / 10;
   std::vector<std::pair<double, double>> filter;
   double theta0 = norm1(e.c);
@@ -588,6 +605,8 @@ int solve_one(Instance& I, double* w, double* lam, int max_iter, double tol, int
   // unscaled objective
   *f_out = e.f / I.fscale;
   for (int i = 0; i < ng; ++i) lam[i] /= I.fscale;
+  if (lamx_out)
+    for (int i = 0; i < nw; ++i) lamx_out[i] = (zU[i] - zL[i]) / I.fscale;
   return status;
 }
 
@@ -643,6 +662,37 @@ int oracle_solve_batch(const oracle_spec* sp, int B, const double* P, int p_stri
     double f = 0;
     int st = solve_one(I, w, lam.data(), sp->max_iter, sp->tol, &it, &f);
     status[b] = st;
+    iters[b] = it;
+    if (f_out) f_out[b] = f;
+    if (lam_g) std::memcpy(lam_g + (size_t)b * ng, lam.data(), sizeof(double) * ng);
+  }
+  return 0;
+}
+
+// Warm-started batched solve: lam0 (B x ng) and lamx0 (B x nw) may be NULL; lamx_out
+// (B x nw) receives the bound multipliers (CasADi convention) if not NULL.
+int oracle_solve_batch_warm(const oracle_spec* sp, int B, const double* P, int p_stride, const double* w0,
+                            const double* lbw, const double* ubw, double mu_init, double bound_push,
+                            double mult_push, const double* lam0, const double* lamx0, double* w_out,
+                            double* lam_g, double* lamx_out, double* f_out, int32_t* status, int32_t* iters,
+                            int nthreads) {
+  const int N = sp->N, nw = 3 + 5 * N, ng = 3 * (N + 1);
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int b = 0; b < B; ++b) {
+    Instance I;
+    setup_instance(I, sp, P + (size_t)b * p_stride, nullptr, lbw, ubw);
+    double* w = w_out + (size_t)b * nw;
+    std::memcpy(w, w0 + (size_t)b * nw, sizeof(double) * nw);
+    Warm wm{mu_init, bound_push, mult_push, lam0 ? lam0 + (size_t)b * ng : nullptr,
+            lamx0 ? lamx0 + (size_t)b * nw : nullptr};
+    std::vector<double> lam(ng);
+    int it = 0;
+    double f = 0;
+    status[b] = solve_one(I, w, lam.data(), sp->max_iter, sp->tol, &it, &f, &wm,
+                          lamx_out ? lamx_out + (size_t)b * nw : nullptr);
     iters[b] = it;
     if (f_out) f_out[b] = f;
     if (lam_g) std::memcpy(lam_g + (size_t)b * ng, lam.data(), sizeof(double) * ng);

@@ -35,6 +35,9 @@ def lib():
         ip = ctypes.POINTER(ctypes.c_int32)
         _LIB.oracle_solve_batch.argtypes = [ctypes.POINTER(OracleSpec), ctypes.c_int, dp, ctypes.c_int, dp, dp, dp,
                                             dp, dp, dp, dp, ip, ip, ctypes.c_int]
+        _LIB.oracle_solve_batch_warm.argtypes = [ctypes.POINTER(OracleSpec), ctypes.c_int, dp, ctypes.c_int, dp, dp,
+                                                 dp, ctypes.c_double, ctypes.c_double, ctypes.c_double, dp, dp,
+                                                 dp, dp, dp, dp, ip, ip, ctypes.c_int]
         _LIB.oracle_stage.argtypes = [ctypes.POINTER(OracleSpec), ctypes.c_int, dp, dp, dp, dp, dp, dp, dp, dp, dp]
     return _LIB
 
@@ -80,6 +83,29 @@ def solve_batch(ocp, P, w0=None, pstage=None, lbw=None, ubw=None, max_iter=200, 
                              _p(lam), _p(f), st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                              it.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), nthreads)
     return {"w": w, "lam_g": lam, "f": f, "status": st, "iters": it}
+
+
+def solve_batch_warm(ocp, P, w0, lam0=None, lamx0=None, mu_init=1e-3, bound_push=1e-3, mult_push=1e-3,
+                     max_iter=200, tol=1e-8, nthreads=0):
+    """IPOPT-style warm start (multipliers + small initial barrier).  Returns w, lam_g, lam_x, f, status, iters."""
+    from . import nlp_ref
+    P = np.ascontiguousarray(P, dtype=np.float64)
+    B = P.shape[0]
+    nw, ng = nlp_ref.n_w(ocp.N), nlp_ref.n_g(ocp.N)
+    lb, ub = nlp_ref.ms_bounds(ocp)
+    lb = np.ascontiguousarray(np.where(np.isfinite(lb), lb, -1e20))
+    ub = np.ascontiguousarray(np.where(np.isfinite(ub), ub, 1e20))
+    w0 = np.ascontiguousarray(w0, dtype=np.float64).reshape(B, nw)
+    l0 = None if lam0 is None else np.ascontiguousarray(lam0, dtype=np.float64).reshape(B, ng)
+    x0 = None if lamx0 is None else np.ascontiguousarray(lamx0, dtype=np.float64).reshape(B, nw)
+    w = np.zeros((B, nw)); lam = np.zeros((B, ng)); lamx = np.zeros((B, nw)); f = np.zeros(B)
+    st = np.zeros(B, np.int32); it = np.zeros(B, np.int32)
+    spec = _spec(ocp, max_iter, tol)
+    ip_ = ctypes.POINTER(ctypes.c_int32)
+    lib().oracle_solve_batch_warm(ctypes.byref(spec), B, _p(P), P.shape[1], _p(w0), _p(lb), _p(ub), mu_init,
+                                  bound_push, mult_push, _p(l0), _p(x0), _p(w), _p(lam), _p(lamx), _p(f),
+                                  st.ctypes.data_as(ip_), it.ctypes.data_as(ip_), nthreads)
+    return {"w": w, "lam_g": lam, "lam_x": lamx, "f": f, "status": st, "iters": it}
 
 
 def stage(ocp, x, u, xr, ur=None, lam=None):

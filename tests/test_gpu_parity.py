@@ -270,3 +270,57 @@ def test_single_shooting_formulation(mpcx, R, golden):
     sol = solver(x0=[0] * (2 * N), lbx=lbw, ubx=ubw, lbg=-math.inf, ubg=math.inf, p=[0, 0, 0, 10, 10, 0])
     assert sol["x"].shape == (2 * N, 1) and sol["g"].shape == (2 * N, 1)
     assert rel_err(sol["x"][0:2, 0], rows2[0, 3:5]) <= REL_TOL
+
+
+# ----------------------------------------------------------------------------- warm start
+def test_warm_start_multipliers(mpcx, R):
+    """IPOPT-style warm start (lam_g0, lam_x0): same optimum, fewer iterations; lam_x
+    from the solver agrees with the stationarity reconstruction from the sweep kernel."""
+    ocp = mpcx.unicycle_point_to_point(N=20)
+    solver = mpcx.nlpsol("s", "mi355x", ocp)
+    P = config2_batch(64, seed=11)
+    cold = solver.solve_batch(P)
+    assert np.all(cold["status"] == 0)
+    lx = solver.lam_x_from_kkt(cold["w"], P, cold["lam_g"])
+    assert np.max(np.abs(lx - cold["lam_x"])) <= 1e-6 * max(1.0, np.max(np.abs(lx)))
+    warm = solver.solve_batch(P, w0=cold["w"], lam_g0=cold["lam_g"], lam_x0=cold["lam_x"])
+    assert np.all(warm["status"] == 0)
+    assert max(rel_err(warm["w"][b], cold["w"][b]) for b in range(64)) <= 1e-6
+    assert warm["iters"].mean() < cold["iters"].mean()
+
+
+def test_device_loop_warm_matches_cold(mpcx, R, C):
+    """Closed loop on the device (solve + plant/shift kernels): the warm-dual loop and the
+    cold-dual loop follow the same trajectory, and the C++ oracle's warm loop agrees."""
+    import torch
+    import bench
+    from mpcx import dist
+    from mpcx.device import DeviceLoop
+
+    ocp = mpcx.unicycle_point_to_point(N=20)
+    solver = mpcx.nlpsol("s", "mi355x", ocp)
+    P0 = dist.config2_inputs(0, 128)
+    loops = [DeviceLoop(solver, P0, warm_duals=wd) for wd in (True, False)]
+    for _ in range(6):
+        for lp in loops:
+            lp.step()
+    torch.cuda.synchronize()
+    Pw, Pc = (lp.P.cpu().numpy() for lp in loops)
+    assert np.max(np.abs(Pw - Pc)) < 1e-6
+    assert np.all(loops[0].status.cpu().numpy() == 0)
+    # oracle loop with the same warm start
+    rocp = R.UnicycleOCP(N=20)
+    P = P0.copy()
+    w0 = bench._cold(P, 20, R)
+    lam0 = lamx0 = None
+    for s in range(6):
+        if s == 0:
+            r = C.solve_batch(rocp, P, w0=w0)
+            r["lam_x"] = np.zeros_like(r["w"])
+        else:
+            r = C.solve_batch_warm(rocp, P, w0, lam0=lam0, lamx0=lamx0, mu_init=1e-4, bound_push=1e-4,
+                                   mult_push=1e-4)
+        P[:, 0:3], _ = R.F(P[:, 0:3], r["w"][:, 3:5], P[:, 3:6], rocp)
+        w0, lam0, lamx0 = bench.shift_np(r["w"], 20), bench.shift_lam_np(r["lam_g"], 20), \
+            bench.shift_lamx_np(r["lam_x"], 20)
+    assert np.max(np.abs(P - Pw)) < 1e-6
