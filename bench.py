@@ -44,8 +44,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024, help="instances per GPU")
-    ap.add_argument("--N", type=int, default=20)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
+                    help="2: point-to-point N=20 B=1024 (headline); 3: circular tracking N=30 B=4096")
+    ap.add_argument("--batch", type=int, default=None, help="instances per GPU (default per config)")
+    ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--roofline-batch", type=int, default=1 << 19)
     ap.add_argument("--roofline-reps", type=int, default=20)
@@ -181,8 +183,10 @@ def main():
     import mpcx
     from mpcx.device import DeviceLoop
 
-    N, B = args.N, args.batch
-    ocp = mpcx.unicycle_point_to_point(N=N)
+    cfg = args.config
+    N = args.N or (20 if cfg == 2 else 30)
+    B = args.batch or (1024 if cfg == 2 else 4096)
+    ocp = mpcx.unicycle_point_to_point(N=N) if cfg == 2 else mpcx.unicycle_tracking(N=N)
     solver = mpcx.nlpsol("bench", "mi355x", ocp, {"ipopt": {"max_iter": 3000}}, device=local)
     stream = torch.cuda.current_stream()
 
@@ -193,10 +197,18 @@ def main():
         return
 
     start, stop = mdist.shard(B, rank)
-    P0 = mdist.config2_inputs(start, stop, args.seed)
+    refs = None
+    if cfg == 2:
+        P0 = mdist.config2_inputs(start, stop, args.seed)
+    else:  # per-step circular references (Trajectory_tracking.py:84-97), precomputed and resident in HBM
+        tau0, P0 = mdist.config3_inputs(start, stop, N=N)
+        refs = torch.from_numpy(np.stack([mpcx.ocp.circular_reference(tau0, t, N).reshape(B, -1)
+                                          for t in range(args.warmup + args.steps)])).to(f"cuda:{local}")
     loop = DeviceLoop(solver, P0, device=f"cuda:{local}", stream=stream)
 
-    for _ in range(args.warmup):
+    for t in range(args.warmup):
+        if refs is not None:
+            loop.set_stage_refs(refs[t])
         loop.step()
     torch.cuda.synchronize()
     K = args.steps
@@ -208,6 +220,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(K):
+        if refs is not None:
+            loop.set_stage_refs(refs[args.warmup + i])
         ev[i][0].record(stream)
         loop.solve(status_out=status_hist[i], iters_out=iters_hist[i])
         ev[i][1].record(stream)
@@ -222,6 +236,8 @@ def main():
 
     # closed-loop statistics: the only collective (RCCL all_gather over xGMI), outside the timed region
     P_fin = loop.P.cpu().numpy()
+    if cfg == 3:  # final error against the stage-0 reference
+        P_fin = np.concatenate([P_fin[:, 0:3], P_fin[:, 3:6]], axis=1)
     S = mdist.stats_matrix(P_fin, None, loop.f.cpu().numpy(), status_hist.max(dim=0).values.cpu().numpy(),
                            iters_hist.cpu().numpy())
     S_all = mdist.all_gather_stats(S, device=loop.P.device)
@@ -229,7 +245,7 @@ def main():
                                           device=loop.P.device)
 
     roof = None
-    if rank == 0 and not args.no_roofline:
+    if rank == 0 and not args.no_roofline and cfg == 2:
         Br = args.roofline_batch
         ms = sweep_roofline(solver, torch, Br, N, args.roofline_reps, stream)
         alg = Br * (SWEEP_BYTES_PER_STAGE * N + SWEEP_BYTES_PER_INSTANCE)
@@ -241,7 +257,7 @@ def main():
                 "bytes_per_launch": alg, "config": f"B={Br}, N={N}"}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and cfg == 2:
         cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
         cores = max(1, min(cores, os.cpu_count() or 1))
         rate, t = cpu_baseline(P0, N, args.cpu_steps, cores)
@@ -256,10 +272,13 @@ def main():
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),
             "ms_per_solve_p50": round(p50, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: SURVEY config-2 generator (global instances 0-83 = golden P_j of Casadi/1exemplo.xlsx)",
-            "config": {"workload": "config 2: closed-loop point-to-point MPC, unicycle, multiple shooting N=20, "
-                                   "RK4 M=4 quadrature cost, IPOPT tol 1e-8", "dynamics": "unicycle", "N": N,
-                       "M": 4, "batch_per_gpu": B, "global_batch": B * world,
+            "data": ("synthetic: SURVEY config-2 generator (global instances 0-83 = golden P_j of Casadi/1exemplo.xlsx)"
+                     if cfg == 2 else "synthetic: SURVEY config-3 generator (phase ~ U[0,20pi), x0 = ref + N(0,0.1^2))"),
+            "config": {"workload": (f"config 2: closed-loop point-to-point MPC, unicycle, multiple shooting N={N}, "
+                                    "RK4 M=4 quadrature cost, IPOPT tol 1e-8") if cfg == 2 else
+                                   (f"config 3: closed-loop circular trajectory tracking (Trajectory_tracking.py), "
+                                    f"unicycle, multiple shooting N={N}, RK4 M=1 node cost, state bounds, tol 1e-8"),
+                       "dynamics": "unicycle", "N": N, "M": ocp.M, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"instance-sharded x{world} (no data-path collective)"},
             "iters_mean": round(float(S_all[:, 1].mean()), 2), "iters_max": int(S_all[:, 2].max()),
             "iters_max_per_step_mean": round(float(iters_max_step), 2),

@@ -78,6 +78,13 @@ class DeviceLoop:
                                       _ptr(self.lam) if d else None, _ptr(self.lam0) if d else None,
                                       _ptr(self.lamx) if d else None, _ptr(self.lamx0) if d else None, s))
 
+    def set_stage_refs(self, refs):
+        """Per-step stage references (tracking, param layout x0_stageref): refs is a
+        (B, N*(nx+nu)) float64 device tensor copied into P[:, nx:] on the loop's stream
+        (Trajectory_tracking.py:105-106 sets solver.par["p", k] each step)."""
+        with torch.cuda.stream(self.stream):
+            self.P[:, 3:].copy_(refs, non_blocking=True)
+
     def step(self):
         self.solve()
         self.shift()

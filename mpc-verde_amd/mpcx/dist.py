@@ -71,6 +71,22 @@ def config2_inputs(start: int, stop: int, seed: int = 20261015, with_golden=True
     return P
 
 
+def config3_inputs(start: int, stop: int, N: int = 30, seed: int = 20261016):
+    """phase tau0 ~ U[0, 20 pi), x0 = ref(tau0) + N(0, 0.1^2 I).
+    Returns (tau0 (n,), P (n, 3 + 5N)) with P = [x0; p_0..p_{N-1}] for step t = 0."""
+    from .ocp import circular_reference
+
+    n = stop - start
+    tau0 = np.zeros(n)
+    x0 = np.zeros((n, 3))
+    for i, g in enumerate(range(start, stop)):
+        rng = np.random.default_rng([seed, g])
+        tau0[i] = rng.uniform(0.0, 20.0 * np.pi)
+        x0[i] = circular_reference(tau0[i:i + 1], 0, 1)[0, 0, 0:3] + rng.normal(scale=0.1, size=3)
+    P = np.concatenate([x0, circular_reference(tau0, 0, N).reshape(n, 5 * N)], axis=1)
+    return tau0, P
+
+
 def stats_matrix(P, w, f, status, iters_hist):
     """Per-instance closed-loop statistics, (B, len(STAT_FIELDS)) float64."""
     B = P.shape[0]

@@ -76,6 +76,22 @@ def unicycle_tracking(N=10, T=0.2):
                x_ub=(20.0, 2.0, math.inf), cost="node", param="x0_stageref")
 
 
+def circular_reference(tau0, t, N, Delta=0.2):
+    """Per-stage references of ``Trajectory Tracking/Trajectory_tracking.py:84-97``.
+
+    For receding-horizon step t and stage k the reference time is
+    tau = tau0 + Delta*(t + k) and p_k = (cos(0.1 tau), sin(0.1 tau), pi/2 + 0.1 tau, 1, 1)
+    (the script's u_ref = (1, 1) is kept as written).  tau0 (B,) offsets the phase per
+    instance (tau0 = 0 is the script's single run).  Returns (B, N, 5).
+    """
+    import numpy as np
+
+    tau0 = np.atleast_1d(np.asarray(tau0, dtype=np.float64))
+    tau = tau0[:, None] + Delta * (t + np.arange(N))[None, :]
+    one = np.ones_like(tau)
+    return np.stack([np.cos(0.1 * tau), np.sin(0.1 * tau), np.pi / 2 + 0.1 * tau, one, one], axis=-1)
+
+
 def to_spec(ocp: OCP, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4)) -> _lib.Spec:
     if ocp.model != "unicycle":
         raise ValueError(f"unsupported model {ocp.model!r}")

@@ -324,3 +324,86 @@ def test_device_loop_warm_matches_cold(mpcx, R, C):
         w0, lam0, lamx0 = bench.shift_np(r["w"], 20), bench.shift_lam_np(r["lam_g"], 20), \
             bench.shift_lamx_np(r["lam_x"], 20)
     assert np.max(np.abs(P - Pw)) < 1e-6
+
+
+# ----------------------------------------------------------------------------- tracking (config 3 family)
+def test_tracking_vs_oracles(mpcx, R, C):
+    """Trajectory_tracking.py's NLP (RK4 M=1, node cost, per-stage reference p_k, state
+    bounds) at config-3 sizes (N=30): GPU vs the C++ IPM oracle (same tol) and vs the
+    independent numpy oracle (tight tol; state bounds verified inactive there)."""
+    from mpcx import dist
+
+    N, B = 30, 256
+    tau0, P = dist.config3_inputs(0, B, N=N)
+    ocp = mpcx.unicycle_tracking(N=N)
+    solver = mpcx.nlpsol("trk", "mi355x", ocp)
+    r = solver.solve_batch(P)
+    assert np.all(r["status"] == 0), np.bincount(r["status"], minlength=4)
+    rocp = R.tracking_ocp(N=N)
+    x0 = P[:, 0:3]
+    ps = P[:, 3:].reshape(B, N, 5)
+    X = np.repeat(x0[:, None], N + 1, axis=1)
+    ref = C.solve_batch(rocp, x0, w0=R.join_w(X, np.zeros((B, N, 2))), pstage=ps)
+    assert np.all(ref["status"] == 0)
+    errs = np.array([rel_err(r["w"][b], ref["w"][b]) for b in range(B)])
+    assert np.mean(errs <= REL_TOL) >= 0.99, np.sort(errs)[-5:]
+    tight = mpcx.nlpsol("trk", "mi355x", ocp, {"ipopt": {"tol": 1e-11}}).solve_batch(P[::32])
+    for i, b in enumerate(range(0, B, 32)):
+        U, Xs, info = R.solve_single_shooting(x0[b], rocp, pstage=ps[b])
+        assert info["status"] == "converged"
+        assert np.all(np.abs(Xs[:, 1]) < 2.0) and np.all(np.abs(Xs[:, 0]) < 20.0)  # state bounds inactive
+        assert rel_err(tight["w"][i], R.join_w(Xs, U)) <= 1e-5
+
+
+def test_tracking_state_bounds_active(mpcx, C, R):
+    """Tracking with an active y-bound: a reference pulled outside y in [-2, 2]."""
+    N, B = 10, 16
+    ocp = mpcx.unicycle_tracking(N=N)
+    rng = np.random.default_rng(5)
+    x0 = np.zeros((B, 3))
+    x0[:, 1] = rng.uniform(0.5, 1.5, B)
+    x0[:, 2] = np.pi / 2
+    ps = np.zeros((B, N, 5))
+    ps[:, :, 1] = 4.0  # y_ref beyond the bound y <= 2
+    ps[:, :, 2] = np.pi / 2
+    ps[:, :, 3] = 1.0
+    P = np.concatenate([x0, ps.reshape(B, -1)], axis=1)
+    r = mpcx.nlpsol("trk", "mi355x", ocp).solve_batch(P)
+    assert np.all(r["status"] == 0)
+    X, U = R.split_w(r["w"], N)
+    assert np.all(X[:, 1:, 1] <= 2.0 + 1e-9) and np.max(X[:, 1:, 1]) > 2.0 - 1e-4  # bound reached, honoured
+    ref = C.solve_batch(R.tracking_ocp(N=N), x0, w0=R.join_w(np.repeat(x0[:, None], N + 1, 1), np.zeros((B, N, 2))),
+                        pstage=ps)
+    assert max(rel_err(r["w"][b], ref["w"][b]) for b in range(B)) <= REL_TOL
+
+
+def test_tracking_closed_loop_facade(mpcx, C, R):
+    """Trajectory_tracking.py's receding-horizon loop (per-step references, shift of the
+    guess, plant) through the façade for 30 steps: follows the C++ oracle loop."""
+    N, steps = 10, 30
+    ocp = mpcx.unicycle_tracking(N=N)
+    solver = mpcx.nlpsol("trk", "mi355x", ocp)
+    F = mpcx.integrator(ocp)
+    rocp = R.tracking_ocp(N=N)
+    x = np.zeros(3)
+    xo = np.zeros(3)
+    w0 = None
+    w0o = R.join_w(np.zeros((1, N + 1, 3)), np.zeros((1, N, 2)))
+    for t in range(steps):
+        p = mpcx.ocp.circular_reference(0.0, t, N)[0]
+        sol = solver(x0=w0, p=np.concatenate([x, p.reshape(-1)]), lbx=solver_bounds(ocp)[0], ubx=solver_bounds(ocp)[1])
+        w = sol["x"][:, 0]
+        x = F(np.concatenate([x, p.reshape(-1)]), w[3:5])[0][:, 0]
+        w0 = np.concatenate([w[5:8], np.concatenate([w[3 + 5 * k:8 + 5 * k] for k in range(1, N)]), w[-5:]])
+        ro = C.solve_batch(rocp, xo[None], w0=w0o, pstage=p[None])
+        xo = R.F(xo, ro["w"][0, 3:5], p[0, 0:3], rocp, p[0, 3:5])[0]
+        wo = ro["w"][0]
+        w0o = np.concatenate([wo[5:8], wo[8:3 + 5 * N], wo[-5:]])[None]
+    assert np.max(np.abs(x - xo)) < 1e-5
+
+
+def solver_bounds(ocp):
+    from oracle import nlp_ref
+
+    lb, ub = nlp_ref.ms_bounds(nlp_ref.tracking_ocp(N=ocp.N))
+    return lb, ub
