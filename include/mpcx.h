@@ -41,7 +41,12 @@ extern "C" {
 typedef struct mpcx_handle mpcx_handle;
 
 enum mpcx_model {
-  MPCX_MODEL_UNICYCLE = 1 /* x=(x,y,theta), u=(v,omega): Casadi/multiple_shooting_casadi.py:68-72 */
+  MPCX_MODEL_UNICYCLE = 1, /* x=(x,y,theta), u=(v,omega): Casadi/multiple_shooting_casadi.py:68-72 */
+  /* x+ = A_j x + B_j u + c_j, l = (z - zr_k)^T W_j (z - zr_k), z = (x, u): the mpctools
+     LTI/LTV QPs (Inverted_pendulum/inverted_pendulum_single_shooting_mpctools.py:19-64,
+     Trajectory Tracking/Trajectory_tracking_dynamic_model.py:117-145); tables set with
+     mpcx_set_linear_model.  (nx, nu) in {(4,1), (5,1)}. */
+  MPCX_MODEL_LINEAR = 2
 };
 
 enum mpcx_cost {
@@ -56,7 +61,8 @@ enum mpcx_param_layout {
   /* p = [x0 (nx); x_ref (nx)]  (n_p = 2 nx, Casadi/multiple_shooting_casadi.py:74,228-231) */
   MPCX_P_X0_XREF = 0,
   /* p = [x0 (nx); (x_ref_k, u_ref_k) for k = 0..N-1]  (n_p = nx + N (nx+nu);
-     Trajectory Tracking/Trajectory_tracking.py:84-97,105-106) */
+     Trajectory Tracking/Trajectory_tracking.py:84-97,105-106).  Always used by
+     MPCX_MODEL_LINEAR (z_ref_k = (x_ref_k, u_ref_k)). */
   MPCX_P_X0_STAGEREF = 1
 };
 
@@ -93,6 +99,7 @@ typedef struct mpcx_spec {
      passed in (lam_g0 / lam_x0 != NULL): initial barrier parameter, primal bound
      push and bound-multiplier push.  Defaults 1e-4. */
   double warm_mu_init, warm_bound_push, warm_mult_push;
+  int32_t nx, nu;       /* state / control dimensions (unicycle: 3, 2) */
 } mpcx_spec;
 
 /* Fill *s with the reference's constants for model/cost at horizon N
@@ -103,6 +110,15 @@ int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N);
 int mpcx_create(const mpcx_spec* s, mpcx_handle** h);
 void mpcx_destroy(mpcx_handle* h);
 const char* mpcx_last_error(void);
+
+/* Tables of an MPCX_MODEL_LINEAR handle (host pointers, copied to the device):
+ *   A n_tab x nx x nx, B n_tab x nx x nu, c n_tab x nx (may be NULL = 0),
+ *   W n_tab x nz(nz+1)/2 packed upper triangle of the stage weight (nz = nx+nu),
+ *   tab tab_rows x N int32 table index of each stage; tab_rows = 1 (shared by all
+ *   instances) or >= the batch size (row b = instance b; LTV schedules).
+ * Call before solving; may be called again (e.g. per closed-loop step). */
+int mpcx_set_linear_model(mpcx_handle* h, int32_t n_tab, const double* A, const double* B, const double* c,
+                          const double* W, const int32_t* tab, int32_t tab_rows);
 
 /* n_w, n_g, n_p of the NLP described by the handle. */
 int mpcx_dims(const mpcx_handle* h, int32_t* n_w, int32_t* n_g, int32_t* n_p);

@@ -30,6 +30,10 @@ struct mpcx_handle {
   int32_t *d_status = nullptr, *d_iters = nullptr;
   size_t cap_sweep = 0;
   double* d_sweep = nullptr;
+  // linear model tables (MPCX_MODEL_LINEAR)
+  double *d_linA = nullptr, *d_linB = nullptr, *d_linc = nullptr, *d_linW = nullptr;
+  int32_t* d_lintab = nullptr;
+  int lin_ntab = 0, lin_rows = 0;
 };
 
 namespace {
@@ -49,6 +53,9 @@ int hipfail(hipError_t e, const char* where) {
     if (e_ != hipSuccess) return hipfail(e_, #expr);   \
   } while (0)
 
+int nx_of(const mpcx_spec& s) { return s.model == MPCX_MODEL_UNICYCLE ? 3 : s.nx; }
+int nu_of(const mpcx_spec& s) { return s.model == MPCX_MODEL_UNICYCLE ? 2 : s.nu; }
+
 mpcx::StageParams stage_params(const mpcx_spec& s) {
   mpcx::StageParams sp;
   sp.T = s.T;
@@ -61,17 +68,17 @@ mpcx::StageParams stage_params(const mpcx_spec& s) {
 }
 
 void spec_bounds(const mpcx_spec& s, std::vector<double>& lb, std::vector<double>& ub) {
-  const int N = s.N, nw = 3 + 5 * N;
+  const int N = s.N, nx = nx_of(s), nu = nu_of(s), nz = nx + nu, nw = nx + nz * N;
   lb.assign(nw, -1e20);
   ub.assign(nw, 1e20);
   for (int k = 0; k < N; ++k) {
-    for (int i = 0; i < 2; ++i) {
-      lb[3 + 5 * k + i] = s.lbu[i];
-      ub[3 + 5 * k + i] = s.ubu[i];
+    for (int i = 0; i < nu; ++i) {
+      lb[nx + nz * k + i] = s.lbu[i];
+      ub[nx + nz * k + i] = s.ubu[i];
     }
-    for (int i = 0; i < 3; ++i) {
-      lb[5 + 5 * k + i] = s.lbx[i];
-      ub[5 + 5 * k + i] = s.ubx[i];
+    for (int i = 0; i < nx; ++i) {
+      lb[nx + nz * k + nu + i] = s.lbx[i];
+      ub[nx + nz * k + nu + i] = s.ubx[i];
     }
   }
 }
@@ -141,6 +148,8 @@ int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N) {
     s->lbx[i] = -1e20;
     s->ubx[i] = 1e20;
   }
+  s->nx = 3;
+  s->nu = 2;
   s->warm_mu_init = 1e-4;
   s->warm_bound_push = 1e-4;
   s->warm_mult_push = 1e-4;
@@ -149,7 +158,9 @@ int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N) {
 
 int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
   if (!s || !out) return fail(MPCX_EINVAL, "null argument");
-  if (s->model != MPCX_MODEL_UNICYCLE) return fail(MPCX_EINVAL, "unknown model");
+  if (s->model != MPCX_MODEL_UNICYCLE && s->model != MPCX_MODEL_LINEAR) return fail(MPCX_EINVAL, "unknown model");
+  if (s->model == MPCX_MODEL_LINEAR && !((s->nx == 4 && s->nu == 1) || (s->nx == 5 && s->nu == 1)))
+    return fail(MPCX_EINVAL, "linear model: (nx, nu) must be (4, 1) or (5, 1)");
   if (s->N < 1 || s->N > 63) return fail(MPCX_EINVAL, "N must be in [1, 63]");
   if (s->M < 1 || s->M > 64) return fail(MPCX_EINVAL, "M must be in [1, 64]");
   if (!(s->T > 0)) return fail(MPCX_EINVAL, "T must be > 0");
@@ -160,10 +171,12 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
   if (!(s->tol > 0)) return fail(MPCX_EINVAL, "tol must be > 0");
   if (!(s->warm_mu_init > 0) || !(s->warm_bound_push > 0) || !(s->warm_mult_push > 0))
     return fail(MPCX_EINVAL, "warm_mu_init / warm_bound_push / warm_mult_push must be > 0");
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < nu_of(*s); ++i)
     if (!(s->lbu[i] < s->ubu[i])) return fail(MPCX_EINVAL, "lbu must be < ubu");
-  for (int i = 0; i < 3; ++i)
+  for (int i = 0; i < nx_of(*s); ++i)
     if (!(s->lbx[i] < s->ubx[i])) return fail(MPCX_EINVAL, "lbx must be < ubx");
+  if (s->model == MPCX_MODEL_LINEAR && s->param_layout != MPCX_P_X0_STAGEREF)
+    return fail(MPCX_EINVAL, "linear model uses param_layout MPCX_P_X0_STAGEREF");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0) return fail(MPCX_EHIP, "no HIP device available");
@@ -171,9 +184,12 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
   HIPCHK(hipSetDevice(s->device));
   mpcx_handle* h = new mpcx_handle();
   h->spec = *s;
-  h->nw = 3 + 5 * s->N;
-  h->ng = 3 * (s->N + 1);
-  h->np = s->param_layout == MPCX_P_X0_XREF ? 6 : 3 + 5 * s->N;
+  h->spec.nx = nx_of(*s);
+  h->spec.nu = nu_of(*s);
+  const int nx = h->spec.nx, nz = nx + h->spec.nu;
+  h->nw = nx + nz * s->N;
+  h->ng = nx * (s->N + 1);
+  h->np = s->param_layout == MPCX_P_X0_XREF ? 2 * nx : nx + nz * s->N;
   std::vector<double> lb, ub;
   spec_bounds(*s, lb, ub);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -209,6 +225,11 @@ void mpcx_destroy(mpcx_handle* h) {
   (void)hipFree(h->d_lamx0);
   (void)hipFree(h->d_lamx);
   (void)hipFree(h->d_sweep);
+  (void)hipFree(h->d_linA);
+  (void)hipFree(h->d_linB);
+  (void)hipFree(h->d_linc);
+  (void)hipFree(h->d_linW);
+  (void)hipFree(h->d_lintab);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -221,11 +242,61 @@ int mpcx_dims(const mpcx_handle* h, int32_t* n_w, int32_t* n_g, int32_t* n_p) {
   return 0;
 }
 
+int mpcx_set_linear_model(mpcx_handle* h, int32_t n_tab, const double* A, const double* B, const double* c,
+                          const double* W, const int32_t* tab, int32_t tab_rows) {
+  if (!h || !A || !B || !W || !tab) return fail(MPCX_EINVAL, "null argument");
+  if (h->spec.model != MPCX_MODEL_LINEAR) return fail(MPCX_EINVAL, "handle is not a linear model");
+  if (n_tab < 1 || tab_rows < 1) return fail(MPCX_EINVAL, "n_tab and tab_rows must be >= 1");
+  const int nx = h->spec.nx, nu = h->spec.nu, nz = nx + nu, nh = nz * (nz + 1) / 2, N = h->spec.N;
+  for (long i = 0; i < (long)tab_rows * N; ++i)
+    if (tab[i] < 0 || tab[i] >= n_tab) return fail(MPCX_EINVAL, "table index out of range at " + std::to_string(i));
+  HIPCHK(hipSetDevice(h->spec.device));
+  (void)hipFree(h->d_linA);
+  (void)hipFree(h->d_linB);
+  (void)hipFree(h->d_linc);
+  (void)hipFree(h->d_linW);
+  (void)hipFree(h->d_lintab);
+  h->d_linA = h->d_linB = h->d_linc = h->d_linW = nullptr;
+  h->d_lintab = nullptr;
+  h->lin_ntab = h->lin_rows = 0;
+  std::vector<double> cz((size_t)n_tab * nx, 0.0);
+  HIPCHK(hipMalloc(&h->d_linA, (size_t)n_tab * nx * nx * sizeof(double)));
+  HIPCHK(hipMalloc(&h->d_linB, (size_t)n_tab * nx * nu * sizeof(double)));
+  HIPCHK(hipMalloc(&h->d_linc, (size_t)n_tab * nx * sizeof(double)));
+  HIPCHK(hipMalloc(&h->d_linW, (size_t)n_tab * nh * sizeof(double)));
+  HIPCHK(hipMalloc(&h->d_lintab, (size_t)tab_rows * N * sizeof(int32_t)));
+  HIPCHK(hipMemcpy(h->d_linA, A, (size_t)n_tab * nx * nx * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->d_linB, B, (size_t)n_tab * nx * nu * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->d_linc, c ? c : cz.data(), (size_t)n_tab * nx * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->d_linW, W, (size_t)n_tab * nh * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->d_lintab, tab, (size_t)tab_rows * N * sizeof(int32_t), hipMemcpyHostToDevice));
+  h->lin_ntab = n_tab;
+  h->lin_rows = tab_rows;
+  return 0;
+}
+
+static int check_model_ready(const mpcx_handle* h, int B) {
+  if (h->spec.model != MPCX_MODEL_LINEAR) return 0;
+  if (!h->d_linA) return fail(MPCX_EINVAL, "linear model tables not set (mpcx_set_linear_model)");
+  if (h->lin_rows > 1 && B > h->lin_rows) return fail(MPCX_EINVAL, "batch larger than the per-instance table rows");
+  return 0;
+}
+
 static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, const double* w0, const double* lam0,
                                  const double* lamx0, const double* lbw, const double* ubw, double* w, double* f,
                                  double* lam, double* lamx, int32_t* st, int32_t* it) {
   mpcx::SolveArgs a;
   a.B = B;
+  a.model = h->spec.model;
+  a.nx = h->spec.nx;
+  a.nu = h->spec.nu;
+  a.lin.A = h->d_linA;
+  a.lin.B = h->d_linB;
+  a.lin.c = h->d_linc;
+  a.lin.W = h->d_linW;
+  a.lin.tab = h->d_lintab;
+  a.lin.per_instance = h->lin_rows > 1 ? 1 : 0;
+  a.lin.n_tab = h->lin_ntab;
   a.N = h->spec.N;
   a.max_iter = h->spec.max_iter;
   a.p_layout = h->spec.param_layout;
@@ -257,6 +328,7 @@ int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const dou
   if (!h || !d_P || !d_w_out) return fail(MPCX_EINVAL, "null argument");
   if (B < 0) return fail(MPCX_EINVAL, "B < 0");
   if (B == 0) return 0;
+  if (int r = check_model_ready(h, B)) return r;
   HIPCHK(hipSetDevice(h->spec.device));
   mpcx::SolveArgs a = make_args(h, B, d_P, d_w0, d_lam_g0, d_lam_x0, h->d_lbw, h->d_ubw, d_w_out, d_f_out, d_lam_g,
                                 d_lam_x, d_status, d_iters);
@@ -271,6 +343,7 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
   if (B < 0) return fail(MPCX_EINVAL, "B < 0");
   if (B == 0) return 0;
   if (int r = check_bounds_vec(h, lbw, ubw)) return r;
+  if (int r = check_model_ready(h, B)) return r;
   HIPCHK(hipSetDevice(h->spec.device));
   if (int r = ensure(h, B)) return r;
   hipStream_t s = h->stream;
@@ -281,7 +354,7 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
     spec_bounds(h->spec, lb, ub);
     if (lbw) lb.assign(lbw, lbw + h->nw);
     if (ubw) ub.assign(ubw, ubw + h->nw);
-    for (int i = 0; i < 3; ++i) {  // X_0 stays free: it is pinned by g_0
+    for (int i = 0; i < h->spec.nx; ++i) {  // X_0 stays free: it is pinned by g_0
       lb[i] = -1e20;
       ub[i] = 1e20;
     }
@@ -310,29 +383,16 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
   if (status) HIPCHK(hipMemcpyAsync(status, h->d_status, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   if (iters) HIPCHK(hipMemcpyAsync(iters, h->d_iters, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  if (g_out) {  // constraint values at the solution (host-side evaluation via the plant kernel)
-    const int N = h->spec.N;
-    std::vector<double> Pst((size_t)B * N * h->np), U((size_t)B * N * 2), XF((size_t)B * N * 3);
-    for (int b = 0; b < B; ++b) {
-      const double* w = w_out + (size_t)b * h->nw;
-      for (int k = 0; k < N; ++k) {
-        double* p = &Pst[((size_t)b * N + k) * h->np];
-        std::memcpy(p, P + (size_t)b * h->np, h->np * sizeof(double));
-        for (int i = 0; i < 3; ++i) p[i] = k == 0 ? w[i] : w[3 + 5 * (k - 1) + 2 + i];
-        if (h->spec.param_layout == MPCX_P_X0_STAGEREF)
-          for (int i = 0; i < 5; ++i) p[3 + i] = P[(size_t)b * h->np + 3 + 5 * k + i];
-        U[((size_t)b * N + k) * 2] = w[3 + 5 * k];
-        U[((size_t)b * N + k) * 2 + 1] = w[3 + 5 * k + 1];
-      }
-    }
-    if (int r = mpcx_plant_step(h, B * N, Pst.data(), U.data(), XF.data(), nullptr)) return r;
-    for (int b = 0; b < B; ++b) {
-      const double* w = w_out + (size_t)b * h->nw;
-      double* g = g_out + (size_t)b * h->ng;
-      for (int i = 0; i < 3; ++i) g[i] = P[(size_t)b * h->np + i] - w[i];
-      for (int k = 0; k < N; ++k)
-        for (int i = 0; i < 3; ++i) g[3 * (k + 1) + i] = XF[((size_t)b * N + k) * 3 + i] - w[3 + 5 * k + 2 + i];
-    }
+  if (g_out) {  // constraint values at the solution (constraints kernel on the device)
+    double* d_g = nullptr;
+    HIPCHK(hipMalloc(&d_g, (size_t)B * h->ng * sizeof(double)));
+    const hipError_t e1 = mpcx::launch_constraints(a, h->d_w, d_g, s);
+    const hipError_t e2 = e1 == hipSuccess ? hipMemcpyAsync(g_out, d_g, (size_t)B * h->ng * sizeof(double),
+                                                            hipMemcpyDeviceToHost, s)
+                                           : e1;
+    const hipError_t e3 = e2 == hipSuccess ? hipStreamSynchronize(s) : e2;
+    (void)hipFree(d_g);
+    HIPCHK(e3);
   }
   return 0;
 }
@@ -340,17 +400,21 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
 int mpcx_plant_step(mpcx_handle* h, int32_t B, const double* P, const double* u, double* xf, double* qf) {
   if (!h || !P || !u || !xf) return fail(MPCX_EINVAL, "null argument");
   if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
+  if (int r = check_model_ready(h, B)) return r;
   HIPCHK(hipSetDevice(h->spec.device));
   hipStream_t s = h->stream;
+  const int nx = h->spec.nx, nu = h->spec.nu;
   double *dP = nullptr, *dU = nullptr, *dX = nullptr, *dQ = nullptr;
   HIPCHK(hipMalloc(&dP, (size_t)B * h->np * sizeof(double)));
-  HIPCHK(hipMalloc(&dU, (size_t)B * 2 * sizeof(double)));
-  HIPCHK(hipMalloc(&dX, (size_t)B * 3 * sizeof(double)));
+  HIPCHK(hipMalloc(&dU, (size_t)B * nu * sizeof(double)));
+  HIPCHK(hipMalloc(&dX, (size_t)B * nx * sizeof(double)));
   HIPCHK(hipMalloc(&dQ, (size_t)B * sizeof(double)));
   HIPCHK(hipMemcpyAsync(dP, P, (size_t)B * h->np * sizeof(double), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(dU, u, (size_t)B * 2 * sizeof(double), hipMemcpyHostToDevice, s));
-  HIPCHK(mpcx::launch_plant(B, h->np, h->spec.param_layout, stage_params(h->spec), dP, dU, dX, dQ, s));
-  HIPCHK(hipMemcpyAsync(xf, dX, (size_t)B * 3 * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(dU, u, (size_t)B * nu * sizeof(double), hipMemcpyHostToDevice, s));
+  mpcx::SolveArgs a = make_args(h, B, dP, nullptr, nullptr, nullptr, h->d_lbw, h->d_ubw, nullptr, nullptr, nullptr,
+                                nullptr, nullptr, nullptr);
+  HIPCHK(mpcx::launch_plant(a, dU, dX, dQ, s));
+  HIPCHK(hipMemcpyAsync(xf, dX, (size_t)B * nx * sizeof(double), hipMemcpyDeviceToHost, s));
   if (qf) HIPCHK(hipMemcpyAsync(qf, dQ, (size_t)B * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   (void)hipFree(dP);
@@ -367,9 +431,12 @@ int mpcx_shift_dev(mpcx_handle* h, int32_t B, double* d_P, const double* d_w, do
   if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
   if ((d_lam_g == nullptr) != (d_lam_g0_next == nullptr) || (d_lam_x == nullptr) != (d_lam_x0_next == nullptr))
     return fail(MPCX_EINVAL, "multiplier shift needs both source and destination");
+  if (int r = check_model_ready(h, B)) return r;
   HIPCHK(hipSetDevice(h->spec.device));
-  HIPCHK(mpcx::launch_shift(B, h->spec.N, h->np, h->spec.param_layout, stage_params(h->spec), d_P, d_w, d_w0_next,
-                            d_lam_g, d_lam_g0_next, d_lam_x, d_lam_x0_next, (hipStream_t)stream));
+  mpcx::SolveArgs a = make_args(h, B, d_P, nullptr, nullptr, nullptr, h->d_lbw, h->d_ubw, nullptr, nullptr, nullptr,
+                                nullptr, nullptr, nullptr);
+  HIPCHK(mpcx::launch_shift(a, d_P, d_w, d_w0_next, d_lam_g, d_lam_g0_next, d_lam_x, d_lam_x0_next,
+                            (hipStream_t)stream));
   return 0;
 }
 
@@ -377,7 +444,8 @@ int mpcx_rk4_sens_dev(mpcx_handle* h, int32_t B, const double* d_X, const double
                       double* d_c, double* d_q, double* d_A, double* d_Bm, double* d_gq, void* stream) {
   if (!h || !d_X || !d_U || !d_xr || !d_c || !d_q || !d_A || !d_Bm || !d_gq) return fail(MPCX_EINVAL, "null argument");
   if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
-  if (h->spec.param_layout != MPCX_P_X0_XREF) return fail(MPCX_EINVAL, "rk4_sens_dev needs param_layout X0_XREF");
+  if (h->spec.model != MPCX_MODEL_UNICYCLE || h->spec.param_layout != MPCX_P_X0_XREF)
+    return fail(MPCX_EINVAL, "rk4_sens_dev: unicycle model with param_layout X0_XREF only");
   HIPCHK(hipSetDevice(h->spec.device));
   HIPCHK(mpcx::launch_rk4_sens(B, h->spec.N, stage_params(h->spec), d_X, d_U, d_xr, d_c, d_q, d_A, d_Bm, d_gq,
                                (hipStream_t)stream));
@@ -388,7 +456,8 @@ int mpcx_rk4_sens(mpcx_handle* h, int32_t B, const double* w, const double* P, d
                   double* Bm, double* gq) {
   if (!h || !w || !P || !c || !q || !A || !Bm || !gq) return fail(MPCX_EINVAL, "null argument");
   if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
-  if (h->spec.param_layout != MPCX_P_X0_XREF) return fail(MPCX_EINVAL, "rk4_sens needs param_layout X0_XREF");
+  if (h->spec.model != MPCX_MODEL_UNICYCLE || h->spec.param_layout != MPCX_P_X0_XREF)
+    return fail(MPCX_EINVAL, "rk4_sens: unicycle model with param_layout X0_XREF only");
   HIPCHK(hipSetDevice(h->spec.device));
   const int N = h->spec.N;
   const size_t nX = (size_t)(N + 1) * 3 * B, nU = (size_t)N * 2 * B, nR = (size_t)3 * B;

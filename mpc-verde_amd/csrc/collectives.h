@@ -1,0 +1,97 @@
+// collectives.h -- lane-group collectives of the fused solve kernel (gfx950, all VALU).
+//
+// A lane group = G contiguous lanes (G = 16/32/64) holding one MPC instance, lane k =
+// shooting node k.  Neighbour moves are DPP wave shifts; all-reduces are DPP within a
+// 16-lane row (quad_perm xor1, quad_perm xor2, row_half_mirror, row_mirror) followed by
+// v_permlane16_swap / v_permlane32_swap across rows.  Every combine is symmetric (a+b on
+// one lane, b+a on its partner), so all lanes of a group end with bit-identical results
+// and take identical control decisions.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mpcx {
+
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int kQuadXor1 = 0xb1, kQuadXor2 = 0x4e, kHalfMirror = 0x141, kMirror = 0x140;
+constexpr int kWaveShl1 = 0x130, kWaveShr1 = 0x138;
+
+struct Pair {
+  double a, b;
+};
+// the two 16-lane rows of each 32-lane half (xor 16), in a fixed order
+__device__ __forceinline__ Pair rows16(double v) {
+  const long long x = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane16_swap((int)(x & 0xffffffffLL), (int)(x & 0xffffffffLL), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((int)(x >> 32), (int)(x >> 32), false, false);
+  return {__longlong_as_double(((long long)hi[0] << 32) | (unsigned int)lo[0]),
+          __longlong_as_double(((long long)hi[1] << 32) | (unsigned int)lo[1])};
+}
+// the two 32-lane halves of the wave (xor 32), in a fixed order
+__device__ __forceinline__ Pair halves32(double v) {
+  const long long x = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((int)(x & 0xffffffffLL), (int)(x & 0xffffffffLL), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((int)(x >> 32), (int)(x >> 32), false, false);
+  return {__longlong_as_double(((long long)hi[0] << 32) | (unsigned int)lo[0]),
+          __longlong_as_double(((long long)hi[1] << 32) | (unsigned int)lo[1])};
+}
+
+struct OpSum {
+  __device__ static double f(double a, double b) { return a + b; }
+};
+struct OpMax {
+  __device__ static double f(double a, double b) { return fmax(a, b); }
+};
+struct OpMin {
+  __device__ static double f(double a, double b) { return fmin(a, b); }
+};
+
+template <int G, class Op>
+__device__ __forceinline__ double greduce(double v) {
+  v = Op::f(v, dpp<kQuadXor1>(v));
+  v = Op::f(v, dpp<kQuadXor2>(v));
+  v = Op::f(v, dpp<kHalfMirror>(v));
+  v = Op::f(v, dpp<kMirror>(v));
+  if (G >= 32) {
+    const Pair p = rows16(v);
+    v = Op::f(p.a, p.b);
+  }
+  if (G >= 64) {
+    const Pair p = halves32(v);
+    v = Op::f(p.a, p.b);
+  }
+  return v;
+}
+template <int G>
+__device__ __forceinline__ double gsum(double v) {
+  return greduce<G, OpSum>(v);
+}
+template <int G>
+__device__ __forceinline__ double gmax(double v) {
+  return greduce<G, OpMax>(v);
+}
+template <int G>
+__device__ __forceinline__ double gmin(double v) {
+  return greduce<G, OpMin>(v);
+}
+// value of lane k+1 / k-1 (whole-wave DPP shift; groups are contiguous and the lanes
+// that would read across a group boundary never use the value)
+__device__ __forceinline__ double from_next(double v) { return dpp<kWaveShl1>(v); }
+__device__ __forceinline__ double from_prev(double v) { return dpp<kWaveShr1>(v); }
+
+// 1/x to full fp64 accuracy: v_rcp_f64 + two Newton steps (no IEEE division sequence
+// on the sequential critical path)
+__device__ __forceinline__ double rcp64(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
+}  // namespace mpcx

@@ -1,0 +1,130 @@
+// models.h -- stage models of the fused solve kernel.
+//
+// A model supplies NX, NU, the structural masks of its Jacobians, a per-lane context
+// (what node k of instance `inst` needs: references, stage matrices) and two stage
+// functions: value (F, q) and derivatives (F, q, A, B, grad q, exact Hessian of
+// fs*q + lam^T F).  The solver kernel (solver.hip) is written once against this.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "riccati.h"
+#include "solver.h"
+#include "unicycle.h"
+
+namespace mpcx {
+
+// ------------------------------------------------------------------------------------
+// Unicycle (Casadi/multiple_shooting_casadi.py:68-114; Trajectory_tracking.py:40-61)
+// A = I + a02 e0 e2^T + a12 e1 e2^T,  B[2][0] = 0  (structural zeros as masks)
+// ------------------------------------------------------------------------------------
+struct UnicycleModel {
+  static constexpr int NX = 3, NU = 2;
+  static constexpr unsigned long long AMASK = (1ull << 0) | (1ull << 2) | (1ull << 4) | (1ull << 5) | (1ull << 8);
+  static constexpr unsigned long long BMASK = (1ull << 0) | (1ull << 1) | (1ull << 2) | (1ull << 3) | (1ull << 5);
+  struct Ctx {
+    double xr[3], ur[2];
+  };
+  __device__ __forceinline__ static void load_ctx(const ModelArgs& a, int inst, const double* P, int k, bool hasU, Ctx& c) {
+    for (int i = 0; i < 3; ++i) c.xr[i] = 0.0;
+    c.ur[0] = c.ur[1] = 0.0;
+    if (a.p_layout == 0) {
+      for (int i = 0; i < 3; ++i) c.xr[i] = P[3 + i];
+    } else if (hasU) {
+      for (int i = 0; i < 3; ++i) c.xr[i] = P[3 + 5 * k + i];
+      for (int i = 0; i < 2; ++i) c.ur[i] = P[3 + 5 * k + 3 + i];
+    }
+  }
+  __device__ __forceinline__ static void derivs(const ModelArgs& a, const Ctx& c, const double* z, const double* ln, double fs,
+                                double* xf, double& q, double* A, double* Bm, double* g, double* H) {
+    const double u2[2] = {z[3], z[4]};
+    uni_derivs<true>(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H);
+  }
+  __device__ __forceinline__ static void value(const ModelArgs& a, const Ctx& c, const double* z, double* xf, double& q) {
+    const double u2[2] = {z[3], z[4]};
+    uni_value(a.sp, z, u2, c.xr, c.ur, xf, q);
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// Linear (time-varying) model with quadratic stage cost -- the mpctools LTI/LTV QPs
+// (Inverted_pendulum/inverted_pendulum_single_shooting_mpctools.py:19-64,
+//  Trajectory Tracking/Trajectory_tracking_dynamic_model.py:117-145):
+//   x+ = A_j x + B_j u + c_j,   l = (z - zr_k)^T W_j (z - zr_k),   z = (x, u),
+// with j = table index of (instance, stage) and zr_k per-stage references in P.
+// ------------------------------------------------------------------------------------
+template <int NX_, int NU_>
+struct LinearModel {
+  static constexpr int NX = NX_, NU = NU_, NZ = NX_ + NU_, NH = NZ * (NZ + 1) / 2;
+  static constexpr unsigned long long AMASK = (NX * NX >= 64) ? ~0ull : ((1ull << (NX * NX)) - 1);
+  static constexpr unsigned long long BMASK = (1ull << (NX * NU)) - 1;
+  struct Ctx {
+    const double *A, *B, *c, *W;
+    double zr[NZ];
+  };
+  __device__ __forceinline__ static void load_ctx(const ModelArgs& a, int inst, const double* P, int k, bool hasU, Ctx& c) {
+    const int N = a.N;
+    int j = 0;
+    if (hasU) j = a.lin.tab[(a.lin.per_instance ? (size_t)inst * N : 0) + k];
+    c.A = a.lin.A + (size_t)j * NX * NX;
+    c.B = a.lin.B + (size_t)j * NX * NU;
+    c.c = a.lin.c + (size_t)j * NX;
+    c.W = a.lin.W + (size_t)j * NH;
+    for (int i = 0; i < NZ; ++i) c.zr[i] = hasU ? P[NX + NZ * k + i] : 0.0;
+  }
+  __device__ __forceinline__ static void value(const ModelArgs& a, const Ctx& c, const double* z, double* xf, double& q) {
+    double dz[NZ];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) dz[i] = z[i] - c.zr[i];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+      double acc = c.c[r];
+#pragma unroll
+      for (int m = 0; m < NX; ++m) acc = fma(c.A[r * NX + m], z[m], acc);
+#pragma unroll
+      for (int l = 0; l < NU; ++l) acc = fma(c.B[r * NU + l], z[NX + l], acc);
+      xf[r] = acc;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+      double wi = 0.0;
+#pragma unroll
+      for (int j = 0; j < NZ; ++j) wi = fma(c.W[symix(i, j, NZ)], dz[j], wi);
+      acc = fma(dz[i], wi, acc);
+    }
+    q = acc;
+  }
+  __device__ __forceinline__ static void derivs(const ModelArgs& a, const Ctx& c, const double* z, const double* ln, double fs,
+                                double* xf, double& q, double* A, double* Bm, double* g, double* H) {
+    double dz[NZ];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) dz[i] = z[i] - c.zr[i];
+#pragma unroll
+    for (int i = 0; i < NX * NX; ++i) A[i] = c.A[i];
+#pragma unroll
+    for (int i = 0; i < NX * NU; ++i) Bm[i] = c.B[i];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+      double acc = c.c[r];
+#pragma unroll
+      for (int m = 0; m < NX; ++m) acc = fma(A[r * NX + m], z[m], acc);
+#pragma unroll
+      for (int l = 0; l < NU; ++l) acc = fma(Bm[r * NU + l], z[NX + l], acc);
+      xf[r] = acc;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+      double wi = 0.0;
+#pragma unroll
+      for (int j = 0; j < NZ; ++j) wi = fma(c.W[symix(i, j, NZ)], dz[j], wi);
+      g[i] = 2.0 * fs * wi;
+      acc = fma(dz[i], wi, acc);
+    }
+    q = acc;
+#pragma unroll
+    for (int i = 0; i < NH; ++i) H[i] = 2.0 * fs * c.W[i];
+  }
+};
+
+}  // namespace mpcx

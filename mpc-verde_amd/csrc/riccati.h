@@ -1,0 +1,179 @@
+// riccati.h -- one backward step of the Riccati factorisation of the barrier KKT system,
+// for a stage with NX states and NU in {1, 2} controls (gfx950 device code).
+//
+// The step is the sequential critical path of the fused solve, so it
+// only computes what the next step needs: the value function (Pn, pn) of node k.  Huu' is
+// factored as L D L^T (no square roots; the two reciprocals are independent), and the
+// feedback K, k_f are recovered afterwards, on all lanes at once (riccati_gains).
+// Structural zeros of A and B are compile-time masks (bit r*NX+j of AMASK = A[r][j] may
+// be non-zero), so a model with sparse Jacobians gets a short step without relying on
+// fast-math folding of x*0.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "collectives.h"
+
+namespace mpcx {
+
+// packed upper-triangular index of a symmetric n x n matrix
+__host__ __device__ constexpr int symix(int i, int j, int n) {
+  return i <= j ? i * n - i * (i - 1) / 2 + (j - i) : j * n - j * (j - 1) / 2 + (i - j);
+}
+
+template <int NX, int NU>
+struct Fac {  // LDL^T data of Huu' kept for the gains (per lane)
+  double r0, r1, t;  // 1/d0, 1/d1, L[1][0]
+  double h0[NX], h1[NX];  // rows of L^{-1} Hux'
+  double g0, g1;          // L^{-1} gu'
+};
+
+template <int NX, int NU, unsigned long long AMASK, unsigned long long BMASK>
+__device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp, const double* A, const double* Bm,
+                                             const double* c, const double* P, const double* p, double* Pn,
+                                             double* pn, Fac<NX, NU>& f) {
+  constexpr int NZ = NX + NU;
+  static_assert(NU == 1 || NU == 2, "NU must be 1 or 2");
+  auto Pm = [&](int i, int j) { return P[symix(i, j, NX)]; };
+  // PA = P A, PB = P B
+  double PA[NX * NX], PB[NX * NU];
+#pragma unroll
+  for (int r = 0; r < NX; ++r) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int m = 0; m < NX; ++m)
+        if (AMASK & (1ull << (m * NX + j))) acc = fma(Pm(r, m), A[m * NX + j], acc);
+      PA[r * NX + j] = acc;
+    }
+#pragma unroll
+    for (int l = 0; l < NU; ++l) {
+      double acc = 0.0;
+#pragma unroll
+      for (int m = 0; m < NX; ++m)
+        if (BMASK & (1ull << (m * NU + l))) acc = fma(Pm(r, m), Bm[m * NU + l], acc);
+      PB[r * NU + l] = acc;
+    }
+  }
+  double Hxx[NX * NX], Hux[NU * NX], Huu[NU * NU];
+#pragma unroll
+  for (int i = 0; i < NX; ++i)
+#pragma unroll
+    for (int j = i; j < NX; ++j) {
+      double acc = Hd[symix(i, j, NZ)];
+#pragma unroll
+      for (int m = 0; m < NX; ++m)
+        if (AMASK & (1ull << (m * NX + i))) acc = fma(A[m * NX + i], PA[m * NX + j], acc);
+      Hxx[i * NX + j] = acc;
+    }
+#pragma unroll
+  for (int l = 0; l < NU; ++l) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      double acc = Hd[symix(j, NX + l, NZ)];
+#pragma unroll
+      for (int m = 0; m < NX; ++m)
+        if (BMASK & (1ull << (m * NU + l))) acc = fma(Bm[m * NU + l], PA[m * NX + j], acc);
+      Hux[l * NX + j] = acc;
+    }
+#pragma unroll
+    for (int n = l; n < NU; ++n) {
+      double acc = Hd[symix(NX + l, NX + n, NZ)];
+#pragma unroll
+      for (int m = 0; m < NX; ++m)
+        if (BMASK & (1ull << (m * NU + l))) acc = fma(Bm[m * NU + l], PB[m * NU + n], acc);
+      Huu[l * NU + n] = acc;
+    }
+  }
+  double s[NX], gx[NX], gu[NU];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    double acc = p[i];
+#pragma unroll
+    for (int m = 0; m < NX; ++m) acc = fma(Pm(i, m), c[m], acc);
+    s[i] = acc;
+  }
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    double acc = gp[i];
+#pragma unroll
+    for (int m = 0; m < NX; ++m)
+      if (AMASK & (1ull << (m * NX + i))) acc = fma(A[m * NX + i], s[m], acc);
+    gx[i] = acc;
+  }
+#pragma unroll
+  for (int l = 0; l < NU; ++l) {
+    double acc = gp[NX + l];
+#pragma unroll
+    for (int m = 0; m < NX; ++m)
+      if (BMASK & (1ull << (m * NU + l))) acc = fma(Bm[m * NU + l], s[m], acc);
+    gu[l] = acc;
+  }
+  bool ok;
+  if constexpr (NU == 1) {
+    const double d0 = Huu[0];
+    ok = d0 > 0.0;
+    f.r0 = rcp64(d0);
+    f.r1 = 0.0;
+    f.t = 0.0;
+    f.g0 = gu[0];
+    f.g1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      f.h0[j] = Hux[j];
+      f.h1[j] = 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const double ri = f.r0 * f.h0[i];
+#pragma unroll
+      for (int j = i; j < NX; ++j) Pn[symix(i, j, NX)] = fma(-ri, f.h0[j], Hxx[i * NX + j]);
+      pn[i] = fma(-ri, f.g0, gx[i]);
+    }
+  } else {
+    const double a = Huu[0], b = Huu[1], d = Huu[3];
+    const double det = fma(a, d, -b * b);
+    ok = (a > 0.0) && (det > 0.0);
+    const double ra = rcp64(a), rdet = rcp64(det);  // independent
+    f.r0 = ra;
+    f.t = b * ra;
+    f.r1 = a * rdet;  // 1 / (d - b^2/a)
+    f.g0 = gu[0];
+    f.g1 = fma(-f.t, gu[0], gu[1]);
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      f.h0[j] = Hux[j];
+      f.h1[j] = fma(-f.t, Hux[j], Hux[NX + j]);
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const double r0i = f.r0 * f.h0[i], r1i = f.r1 * f.h1[i];
+#pragma unroll
+      for (int j = i; j < NX; ++j) Pn[symix(i, j, NX)] = fma(-r1i, f.h1[j], fma(-r0i, f.h0[j], Hxx[i * NX + j]));
+      pn[i] = fma(-r1i, f.g1, fma(-r0i, f.g0, gx[i]));
+    }
+  }
+  return ok;
+}
+
+// K = -Huu'^{-1} Hux', kf = -Huu'^{-1} gu' from the LDL^T data (off the critical path).
+template <int NX, int NU>
+__device__ __forceinline__ void riccati_gains(const Fac<NX, NU>& f, double* K, double* kf) {
+  if constexpr (NU == 1) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) K[j] = -f.r0 * f.h0[j];
+    kf[0] = -f.r0 * f.g0;
+  } else {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const double y1 = f.r1 * f.h1[j];
+      K[NX + j] = -y1;
+      K[j] = -fma(f.r0, f.h0[j], -f.t * y1);
+    }
+    const double z1 = f.r1 * f.g1;
+    kf[1] = -z1;
+    kf[0] = -fma(f.r0, f.g0, -f.t * z1);
+  }
+}
+
+}  // namespace mpcx

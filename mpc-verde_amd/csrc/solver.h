@@ -7,11 +7,24 @@
 
 namespace mpcx {
 
+// Tables of the linear model (MPCX_MODEL_LINEAR), device memory owned by the handle.
+struct LinTables {
+  const double* A;    // n_tab x NX*NX (row-major)
+  const double* B;    // n_tab x NX*NU
+  const double* c;    // n_tab x NX
+  const double* W;    // n_tab x NZ(NZ+1)/2 (packed upper triangle, z = (x, u))
+  const int32_t* tab; // N (shared) or rows x N (per instance) table indices
+  int per_instance;
+  int n_tab;
+};
+
 struct SolveArgs {
   int B, N, max_iter, p_layout;
   int p_stride;
+  int model, nx, nu;
   double tol;
-  StageParams sp;
+  StageParams sp;       // unicycle constants
+  LinTables lin;        // linear model tables
   const double* P;      // B x p_stride (device)
   const double* w0;     // B x nw or null (cold start: X_k = x0, U = 0)
   const double* lam0;   // B x ng initial constraint multipliers or null
@@ -28,12 +41,24 @@ struct SolveArgs {
   int32_t* iters;       // B or null
 };
 
+// What a stage model reads (a local copy: taking the address of the kernel argument
+// struct itself would force it onto the scratch stack).
+struct ModelArgs {
+  StageParams sp;
+  LinTables lin;
+  int p_layout, N;
+};
+__host__ __device__ inline ModelArgs model_args(const SolveArgs& a) { return ModelArgs{a.sp, a.lin, a.p_layout, a.N}; }
+
 hipError_t launch_solve(const SolveArgs& a, hipStream_t stream);
 hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X, const double* U, const double* XR,
                            double* C, double* Q, double* A, double* Bm, double* G, hipStream_t stream);
-hipError_t launch_plant(int B, int p_stride, int p_layout, const StageParams& sp, const double* P, const double* U,
-                        double* XF, double* QF, hipStream_t stream);
-hipError_t launch_shift(int B, int N, int p_stride, int p_layout, const StageParams& sp, double* P, const double* W,
-                        double* W0, const double* L, double* L0, const double* LX, double* LX0, hipStream_t stream);
+// plant: x+ = F(x0, u) for B instances (stage-0 model of each instance)
+hipError_t launch_plant(const SolveArgs& a, const double* U, double* XF, double* QF, hipStream_t stream);
+// closed-loop shift (plant + shifted warm start of primal and multipliers)
+// constraint values g (B x ng) at w
+hipError_t launch_constraints(const SolveArgs& a, const double* W, double* Gout, hipStream_t stream);
+hipError_t launch_shift(const SolveArgs& a, double* P, const double* W, double* W0, const double* L, double* L0,
+                        const double* LX, double* LX0, hipStream_t stream);
 
 }  // namespace mpcx

@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPCX_LIB", os.path.join(_HERE, "libmpcx.so"))
 
 MODEL_UNICYCLE = 1
+MODEL_LINEAR = 2
 COST_QUADRATURE = 0
 COST_NODE = 1
 P_X0_XREF = 0
@@ -24,7 +25,8 @@ STATUS = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Maximum_Ite
 
 # C-ABI entry points (include/mpcx.h) -- checked by tests/test_capi_symbols.py
 EXPORTS = ("mpcx_default_spec", "mpcx_create", "mpcx_destroy", "mpcx_last_error", "mpcx_dims", "mpcx_solve_batch",
-           "mpcx_solve_batch_dev", "mpcx_plant_step", "mpcx_shift_dev", "mpcx_rk4_sens", "mpcx_rk4_sens_dev")
+           "mpcx_solve_batch_dev", "mpcx_plant_step", "mpcx_shift_dev", "mpcx_rk4_sens", "mpcx_rk4_sens_dev",
+           "mpcx_set_linear_model")
 
 
 class Spec(ctypes.Structure):
@@ -36,7 +38,8 @@ class Spec(ctypes.Structure):
                 ("tol", ctypes.c_double), ("Q", ctypes.c_double * 8), ("R", ctypes.c_double * 8),
                 ("lbu", ctypes.c_double * 8), ("ubu", ctypes.c_double * 8), ("lbx", ctypes.c_double * 8),
                 ("ubx", ctypes.c_double * 8), ("warm_mu_init", ctypes.c_double),
-                ("warm_bound_push", ctypes.c_double), ("warm_mult_push", ctypes.c_double)]
+                ("warm_bound_push", ctypes.c_double), ("warm_mult_push", ctypes.c_double),
+                ("nx", ctypes.c_int32), ("nu", ctypes.c_int32)]
 
 
 _lib = None
@@ -94,6 +97,7 @@ def load():
     lib.mpcx_shift_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mpcx_rk4_sens.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp, dp, dp, dp]
     lib.mpcx_rk4_sens_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.mpcx_set_linear_model.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp, ip, ctypes.c_int32]
     for name in EXPORTS:
         getattr(lib, name)  # AttributeError if an export is missing
     _lib = lib

@@ -102,6 +102,7 @@ def to_spec(ocp: OCP, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4)
     s.N, s.M, s.max_iter, s.device = int(ocp.N), int(ocp.M), int(max_iter), int(device)
     s.T, s.tol = float(ocp.T), float(tol)
     s.warm_mu_init, s.warm_bound_push, s.warm_mult_push = (float(v) for v in warm)
+    s.nx, s.nu = 3, 2
     big = 1e20
 
     def fin(v, default):

@@ -50,8 +50,8 @@ def test_python_binding_matches_header():
     import mpcx
 
     assert set(mpcx._lib.EXPORTS) == set(declared_symbols())
-    # struct layout: 8 int32 + 2 double + 6 x double[8] + 3 double (warm start)
-    assert ctypes.sizeof(mpcx._lib.Spec) == 8 * 4 + 2 * 8 + 6 * 8 * 8 + 3 * 8
+    # struct layout: 8 int32 + 2 double + 6 x double[8] + 3 double (warm start) + 2 int32 (nx, nu)
+    assert ctypes.sizeof(mpcx._lib.Spec) == 8 * 4 + 2 * 8 + 6 * 8 * 8 + 3 * 8 + 2 * 4
 
 
 def test_default_spec_without_gpu(lib):
