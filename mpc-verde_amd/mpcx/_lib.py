@@ -141,6 +141,15 @@ class Handle:
     def ptr(self):
         return self._h
 
+    def set_linear_model(self, lin):
+        """Upload the stage tables of a LinearOCP (mpcx_set_linear_model)."""
+        n_tab, A, B, c, Wp, tab, rows = lin.tables()
+        A, B, c, Wp = (np.ascontiguousarray(v, np.float64) for v in (A, B, c, Wp))
+        tab = np.ascontiguousarray(tab, np.int32)
+        check(load().mpcx_set_linear_model(self._h, int(n_tab), dptr(A), dptr(B), dptr(c), dptr(Wp), iptr(tab),
+                                           int(rows)))
+        self._lin_refs = (A, B, c, Wp, tab)
+
     @property
     def spec(self):
         return self._spec

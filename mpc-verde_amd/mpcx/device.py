@@ -83,7 +83,7 @@ class DeviceLoop:
         (B, N*(nx+nu)) float64 device tensor copied into P[:, nx:] on the loop's stream
         (Trajectory_tracking.py:105-106 sets solver.par["p", k] each step)."""
         with torch.cuda.stream(self.stream):
-            self.P[:, 3:].copy_(refs, non_blocking=True)
+            self.P[:, self.solver.ocp.nx:].copy_(refs, non_blocking=True)
 
     def step(self):
         self.solve()

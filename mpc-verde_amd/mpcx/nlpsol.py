@@ -27,6 +27,7 @@ import time
 import numpy as np
 
 from . import _lib
+from .lti import LinearOCP
 from .ocp import OCP, to_spec
 
 
@@ -60,7 +61,17 @@ class Solver:
         if ip:
             raise ValueError(f"unsupported ipopt options: {sorted(ip)}")
         self._h = _lib.Handle(to_spec(ocp, self.max_iter, self.tol, device))
+        if ocp.model == "linear":
+            self._h.set_linear_model(ocp)
         self._stats = {}
+
+    def set_linear_model(self, lin=None):
+        """Re-upload stage tables (LTV: new tables or per-instance schedule for the next step)."""
+        if lin is not None:
+            if lin.model != "linear" or (lin.nx, lin.nu, lin.N) != (self.ocp.nx, self.ocp.nu, self.ocp.N):
+                raise ValueError("set_linear_model: incompatible problem")
+            self.ocp = lin
+        self._h.set_linear_model(self.ocp)
 
     # ---------------------------------------------------------------- layout
     @property
@@ -115,6 +126,8 @@ class Solver:
 
     def rk4_sens(self, w, P):
         """Per-interval defects, costs and Jacobians at w (B, n_w) -- the sweep kernel."""
+        if self.ocp.model != "unicycle":
+            raise ValueError("rk4_sens: the sweep kernel evaluates the unicycle model only")
         w = np.ascontiguousarray(np.atleast_2d(np.asarray(w, np.float64)))
         P = np.ascontiguousarray(np.atleast_2d(np.asarray(P, np.float64)))
         B, N = w.shape[0], self.ocp.N
@@ -154,6 +167,8 @@ class Solver:
         ubx = _vec(ubx, self.n_w, "ubx", math.inf)
         lbg = _vec(lbg, self.n_g, "lbg", 0.0 if not ss else -math.inf)
         ubg = _vec(ubg, self.n_g, "ubg", 0.0 if not ss else math.inf)
+        if ss and ocp.model != "unicycle":
+            raise ValueError("single shooting is mapped for the unicycle model only")
         if ss:
             if np.any(np.isfinite(lbg)) or np.any(np.isfinite(ubg)):
                 raise ValueError("single shooting: only inactive (+-inf) bounds on g are supported")
@@ -212,6 +227,9 @@ class Solver:
 class Integrator:
     """``F = ca.Function('F', [P, U], [X, Q], ['x0','p'], ['xf','qf'])`` (:114).
 
+    For a LinearOCP this is stage 0's map x+ = A_j x + B_j u + c_j, q = l_0 (the
+    reference's discrete ``f``, e.g. ``inverted_pendulum...py:24-28``).
+
     ``F(p, u)`` -> [xf (3,1), qf (1,1)];  ``F(x0=p, p=u)`` -> {'xf', 'qf'};
     ``F.batch(P, U)`` -> (xf (B,3), qf (B,)).  Evaluated by the plant kernel.
     """
@@ -219,14 +237,17 @@ class Integrator:
     def __init__(self, ocp: OCP, device: int = 0, handle=None):
         self.ocp = ocp
         self._h = handle if handle is not None else _lib.Handle(to_spec(ocp, device=device))
+        if handle is None and ocp.model == "linear":
+            self._h.set_linear_model(ocp)
 
     def batch(self, P, U):
         P = np.ascontiguousarray(np.atleast_2d(np.asarray(P, np.float64)))
         U = np.ascontiguousarray(np.atleast_2d(np.asarray(U, np.float64)))
         B = P.shape[0]
-        if U.shape != (B, 2):
-            raise ValueError("U must be (B, 2)")
-        xf = np.empty((B, 3))
+        nx, nu = self.ocp.nx, self.ocp.nu
+        if U.shape != (B, nu):
+            raise ValueError(f"U must be (B, {nu})")
+        xf = np.empty((B, nx))
         qf = np.empty(B)
         _lib.check(_lib.load().mpcx_plant_step(self._h.ptr, B, _lib.dptr(P), _lib.dptr(U), _lib.dptr(xf),
                                                _lib.dptr(qf)))
@@ -236,10 +257,10 @@ class Integrator:
         if kw:
             p = kw.get("x0")
             u = kw.get("p")
-            xf, qf = self.batch(_vec(p, self._h.n_p, "x0")[None, :], _vec(u, 2, "p")[None, :])
+            xf, qf = self.batch(_vec(p, self._h.n_p, "x0")[None, :], _vec(u, self.ocp.nu, "p")[None, :])
             return {"xf": xf[0][:, None], "qf": qf[:, None]}
         p, u = args
-        xf, qf = self.batch(_vec(p, self._h.n_p, "p")[None, :], _vec(u, 2, "u")[None, :])
+        xf, qf = self.batch(_vec(p, self._h.n_p, "p")[None, :], _vec(u, self.ocp.nu, "u")[None, :])
         return [xf[0][:, None], qf[:, None]]
 
 
@@ -247,8 +268,8 @@ def nlpsol(name: str, plugin: str, prob: OCP, opts: dict | None = None, device: 
     """Create a solver (``ca.nlpsol`` signature).  plugin must be 'mi355x'."""
     if plugin not in ("mi355x",):
         raise ValueError(f"unknown plugin {plugin!r} (available: 'mi355x')")
-    if not isinstance(prob, OCP):
-        raise TypeError("prob must be an mpcx.OCP (symbolic CasADi problems are not supported)")
+    if not isinstance(prob, (OCP, LinearOCP)):
+        raise TypeError("prob must be an mpcx.OCP or mpcx.LinearOCP (symbolic CasADi problems are not supported)")
     return Solver(name, prob, opts, device)
 
 

@@ -92,28 +92,33 @@ def circular_reference(tau0, t, N, Delta=0.2):
     return np.stack([np.cos(0.1 * tau), np.sin(0.1 * tau), np.pi / 2 + 0.1 * tau, one, one], axis=-1)
 
 
-def to_spec(ocp: OCP, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4)) -> _lib.Spec:
-    if ocp.model != "unicycle":
+def to_spec(ocp, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4)) -> _lib.Spec:
+    """mpcx_spec of an :class:`OCP` (unicycle) or :class:`mpcx.lti.LinearOCP` (linear model;
+    its stage tables are uploaded separately by the solver, mpcx_set_linear_model)."""
+    if ocp.model not in ("unicycle", "linear"):
         raise ValueError(f"unsupported model {ocp.model!r}")
     s = _lib.Spec()
-    s.model = _lib.MODEL_UNICYCLE
+    lin = ocp.model == "linear"
+    s.model = _lib.MODEL_LINEAR if lin else _lib.MODEL_UNICYCLE
     s.cost = {"quadrature": _lib.COST_QUADRATURE, "node": _lib.COST_NODE}[ocp.cost]
     s.param_layout = {"x0_xref": _lib.P_X0_XREF, "x0_stageref": _lib.P_X0_STAGEREF}[ocp.param]
-    s.N, s.M, s.max_iter, s.device = int(ocp.N), int(ocp.M), int(max_iter), int(device)
+    s.N, s.M, s.max_iter, s.device = int(ocp.N), int(getattr(ocp, "M", 1)), int(max_iter), int(device)
     s.T, s.tol = float(ocp.T), float(tol)
     s.warm_mu_init, s.warm_bound_push, s.warm_mult_push = (float(v) for v in warm)
-    s.nx, s.nu = 3, 2
+    s.nx, s.nu = int(ocp.nx), int(ocp.nu)
     big = 1e20
 
     def fin(v, default):
         return default if not math.isfinite(v) else float(v)
 
-    for i in range(3):
-        s.Q[i] = float(ocp.Q[i])
+    for i in range(ocp.nx):
+        if not lin:
+            s.Q[i] = float(ocp.Q[i])
         s.lbx[i] = fin(ocp.x_lb[i], -big)
         s.ubx[i] = fin(ocp.x_ub[i], big)
-    for i in range(2):
-        s.R[i] = float(ocp.R[i])
-        s.lbu[i] = float(ocp.u_lb[i])
-        s.ubu[i] = float(ocp.u_ub[i])
+    for i in range(ocp.nu):
+        if not lin:
+            s.R[i] = float(ocp.R[i])
+        s.lbu[i] = fin(ocp.u_lb[i], -big)
+        s.ubu[i] = fin(ocp.u_ub[i], big)
     return s

@@ -423,3 +423,136 @@ def kkt_residual_ms(w, lam_g, P, ocp, pstage=None):
     pg = w - np.clip(w - grad, lb, ub)
     _, gval = ms_functions(np.asarray(w), P, ocp, pstage)
     return float(np.max(np.abs(pg))), float(np.max(np.abs(gval)))
+
+
+# ----------------------------------------------------------------------------
+# LTI cart-pole QP with move blocking (config 5 family)
+# Inverted_pendulum/inverted_pendulum_single_shooting_mpctools.py:15-78
+# ----------------------------------------------------------------------------
+
+
+def pendulum_model(T=0.01):
+    """Ac = M^T (:19-20), Bc (:22), zero-order-hold c2d (mpctools util.c2d, :24)."""
+    from scipy.linalg import expm
+
+    Ac = np.array([[0, 0, 0, 0], [1, -10, 0, -20], [0, 9.81, 0, 39.24], [0, 0, 1, 0]], float).T
+    Bc = np.array([[0.0], [1.0], [0.0], [2.0]])
+    Mx = np.zeros((5, 5))
+    Mx[:4, :4] = Ac
+    Mx[:4, 4:] = Bc
+    E = expm(Mx * T)
+    return E[:4, :4], E[:4, 4:]
+
+
+def pendulum_qp_solve(x0, A, Bd, N=50, n_free=5, uprev=0.0, umax=200.0, xt=(10.0, 0, 0, 0), q1=1.2, q3=1.0,
+                      r=0.01, tol=1e-12):
+    """The per-step QP of :34-64 condensed onto the n_free free moves (u_k = u_{n_free-1}
+    for k >= n_free, Du = 0 there, :32-42): min sum_{k<N} (q1(x1-xt1))^2 + (q3 x3)^2 + (r Du_k)^2
+    with |u| <= umax, Du_0 = u_0 - uprev.  Exact projected-Newton solve (convex QP).
+    Returns u (n_free,)."""
+    x0 = np.asarray(x0, float)
+    # x_k = A^k x0 + S_k u over the free moves u; u_k = E_k u (E_k selects move min(k, n_free-1))
+    nx = 4
+    E = np.zeros((N, n_free))
+    for k in range(N):
+        E[k, min(k, n_free - 1)] = 1.0
+    Sx = np.zeros((N, nx, n_free))
+    fx = np.zeros((N, nx))
+    x = x0.copy()
+    S = np.zeros((nx, n_free))
+    for k in range(N):
+        fx[k] = x
+        Sx[k] = S
+        x = A @ x
+        S = A @ S + np.outer(Bd[:, 0], E[k])
+    # cost terms: rows of residual vector r(u) = R u + c
+    rows, cs = [], []
+    for k in range(N):
+        rows.append(q1 * Sx[k, 0]); cs.append(q1 * (fx[k, 0] - xt[0]))
+        rows.append(q3 * Sx[k, 2]); cs.append(q3 * fx[k, 2])
+        d = E[k] - (E[k - 1] if k > 0 else 0 * E[0])
+        rows.append(r * d); cs.append(-r * uprev if k == 0 else 0.0)
+    Rm = np.array(rows)
+    c = np.array(cs)
+    H = 2 * Rm.T @ Rm
+    g0 = 2 * Rm.T @ c
+    lb, ub = -umax * np.ones(n_free), umax * np.ones(n_free)
+    u = np.clip(np.linalg.solve(H, -g0), lb, ub)
+    for _ in range(100):
+        g = H @ u + g0
+        act = ((u <= lb) & (g > 0)) | ((u >= ub) & (g < 0))
+        fr = ~act
+        un = u.copy()
+        if fr.any():
+            un[fr] = np.linalg.solve(H[np.ix_(fr, fr)], -(g0[fr] + H[np.ix_(fr, act)] @ u[act]))
+        un = np.clip(un, lb, ub)
+        if np.max(np.abs(un - u)) <= tol * max(1.0, np.max(np.abs(u))):
+            u = un
+            break
+        u = un
+    return u
+
+
+def pendulum_closed_loop(nsim=1000, T=0.01, N=50):
+    """:66-78 -- x0 = 0; each step solve, apply u_0, x <- A x + B u (uprev stays 0 as in the script)."""
+    A, Bd = pendulum_model(T)
+    x = np.zeros(4)
+    xs = [x.copy()]
+    us = []
+    for _ in range(nsim):
+        u = pendulum_qp_solve(x, A, Bd, N=N)[0]
+        us.append(u)
+        x = A @ x + Bd[:, 0] * u
+        xs.append(x.copy())
+    return np.array(xs), np.array(us)
+
+
+def lq_solve(x0, A, B, c, W, tab, zr, lbu, ubu, x_lb=None, x_ub=None, tol=1e-13):
+    """Generic table-driven linear-quadratic OCP (the model of mpcx MPCX_MODEL_LINEAR):
+    x_{k+1} = A_j x_k + B_j u_k + c_j, J = sum_k (z_k - zr_k)^T W_j (z_k - zr_k), j = tab[k],
+    lbu <= u_k <= ubu, condensed onto U and solved exactly by projected Newton.
+    State bounds are not supported here (use x_lb/x_ub = None).  Returns (X (N+1,nx), U (N,nu), J)."""
+    x0 = np.asarray(x0, float)
+    N = len(tab)
+    nx, nu = A.shape[-1], B.shape[-1]
+    nz = nx + nu
+    nU = N * nu
+    # x_k = fx[k] + Sx[k] U
+    fx = np.zeros((N + 1, nx))
+    Sx = np.zeros((N + 1, nx, nU))
+    fx[0] = x0
+    for k in range(N):
+        j = tab[k]
+        fx[k + 1] = A[j] @ fx[k] + c[j]
+        Sx[k + 1] = A[j] @ Sx[k]
+        Sx[k + 1][:, k * nu:(k + 1) * nu] += B[j]
+    H = np.zeros((nU, nU))
+    g0 = np.zeros(nU)
+    const = 0.0
+    for k in range(N):
+        j = tab[k]
+        Sz = np.zeros((nz, nU))
+        Sz[:nx] = Sx[k]
+        Sz[nx:, k * nu:(k + 1) * nu] = np.eye(nu)
+        fz = np.concatenate([fx[k], np.zeros(nu)]) - zr[k]
+        H += 2 * Sz.T @ W[j] @ Sz
+        g0 += 2 * Sz.T @ W[j] @ fz
+        const += fz @ W[j] @ fz
+    lb = np.tile(np.asarray(lbu, float), N)
+    ub = np.tile(np.asarray(ubu, float), N)
+    u = np.clip(np.linalg.solve(H, -g0), lb, ub)
+    for _ in range(200):
+        g = H @ u + g0
+        act = ((u <= lb) & (g > 0)) | ((u >= ub) & (g < 0))
+        fr = ~act
+        un = u.copy()
+        if fr.any():
+            un[fr] = np.linalg.solve(H[np.ix_(fr, fr)], -(g0[fr] + H[np.ix_(fr, act)] @ u[act]))
+        un = np.clip(un, lb, ub)
+        if np.max(np.abs(un - u)) <= tol * max(1.0, np.max(np.abs(u))):
+            u = un
+            break
+        u = un
+    X = fx + np.einsum("kij,j->ki", Sx, u)
+    J = 0.5 * u @ H @ u + g0 @ u + const
+    return X, u.reshape(N, nu), J

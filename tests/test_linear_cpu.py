@@ -1,0 +1,109 @@
+"""CPU tests of the linear-model family.
+
+* the pendulum oracle (oracle/nlp_ref.py pendulum_*) reproduces the reference's own
+  closed loop ``Inverted_pendulum/invertpend_data_py.xlsx`` (tests/golden/pendulum_N50_golden.json);
+* the product's host-side tables (mpcx/lti.py: c2d, u_prev augmentation, move blocking)
+  give, through the generic LQ oracle, the same optimum as the pinned pendulum oracle;
+* the LTV lateral builder's references follow the script's as-written rules.
+No GPU is touched.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+@pytest.fixture(scope="module")
+def pend_golden():
+    with open(os.path.join(ROOT, "tests", "golden", "pendulum_N50_golden.json")) as f:
+        return np.array(json.load(f)["rows"])
+
+
+def test_pendulum_oracle_closed_loop_matches_golden(pend_golden):
+    from oracle import nlp_ref as R
+
+    xs, us = R.pendulum_closed_loop(nsim=1000)
+    assert pend_golden.shape == (1001, 6)
+    assert np.abs(xs - pend_golden[:, 0:4]).max() <= 1e-9
+    assert np.abs(us - pend_golden[:1000, 4]).max() <= 1e-8 * np.abs(pend_golden[:, 4]).max()
+    assert abs(us[0] - (-60.84425718936204)) < 1e-9
+
+
+def test_pendulum_tables_match_pinned_oracle():
+    from oracle import nlp_ref as R
+    from mpcx import lti
+
+    lin = lti.inverted_pendulum_qp()
+    A, Bd = R.pendulum_model()
+    np.testing.assert_array_equal(lin.A_plant, A)
+    np.testing.assert_array_equal(lin.B_plant, Bd)
+    assert lin.nx == 5 and lin.nu == 1 and lin.n_tab == 2 and list(lin.tab[:6]) == [0, 0, 0, 0, 0, 1]
+    rng = np.random.default_rng(3)
+    for scale in (1.0, 30.0):  # 30: bounds |u| <= 200 active
+        x = scale * rng.uniform([-1, -.5, -.2, -.5], [1, .5, .2, .5])
+        up = float(rng.uniform(-50, 50))
+        u_ref = R.pendulum_qp_solve(x, A, Bd, uprev=up)
+        P = lti.pendulum_params(lin, x, up)[0]
+        X, U, _ = R.lq_solve(P[:5], lin.A, lin.B, lin.c, lin.W, lin.tab, P[5:].reshape(50, 6), [-200], [200])
+        assert np.abs(U[:5, 0] - u_ref).max() <= 1e-9 * max(1.0, np.abs(u_ref).max())
+        assert np.abs(U[5:, 0]).max() <= 1e-9  # blocked stages' dummy input
+        assert np.abs(X[5:, 4] - u_ref[4]).max() <= 1e-9 * max(1.0, abs(u_ref[4]))  # u_prev carries u_4
+        if scale > 1:
+            assert np.any(np.abs(u_ref) >= 200 - 1e-9)
+
+
+def test_pack_sym_matches_symix():
+    from mpcx import lti
+
+    n = 6
+    W = np.arange(n * n, dtype=float).reshape(n, n)
+    W = W + W.T
+    p = lti.pack_sym(W)
+
+    def symix(i, j):
+        if i > j:
+            i, j = j, i
+        return i * n - i * (i - 1) // 2 + (j - i)
+
+    for i in range(n):
+        for j in range(n):
+            assert p[symix(i, j)] == W[i, j]
+
+
+def test_lateral_ltv_builder_and_refs():
+    from mpcx import lti
+    import csv
+
+    with open(os.path.join(ROOT, "tests", "golden", "lane_change.csv")) as f:
+        rows = [tuple(float(v) for v in r.values()) for r in csv.DictReader(f)]
+    xr, yr, vr = (np.array(c) for c in zip(*rows))
+    assert len(vr) == 500
+    par = lti.lateral_references(xr, yr, vr, Delta=0.05, horizon=10)
+    assert par.shape == (500, 10, 5) and np.all(np.isfinite(par))
+    # clamp at veclim = 499 (:94-97)
+    np.testing.assert_array_equal(par[495, 9, 0:3], [yr[499], np.arctan2(yr[499], xr[499]), vr[499]])
+    # centred difference in the interior (:112-113)
+    t, k = 10, 3
+    assert par[t, k, 3] == pytest.approx((np.arctan2(yr[k + 1 + t], xr[k + 1 + t]) - par[t - 1, k, 1]) / 0.1)
+    lin = lti.lateral_ltv(N=10, Delta=0.05, vref=vr[:3], per_instance_tab=[0, 1, 2, 2])
+    assert lin.tab.shape == (4, 10) and lin.n_tab == 3
+    Ac, Bc = lti.lateral_continuous(vr[1])
+    A, Bd = lti.c2d(Ac, Bc, 0.05)
+    np.testing.assert_allclose(lin.A[1], A, rtol=0, atol=0)
+    # ZOH: A = expm(Ac T) satisfies the semigroup property
+    A2, _ = lti.c2d(Ac, Bc, 0.1)
+    np.testing.assert_allclose(A @ A, A2, rtol=1e-10, atol=1e-12)
+
+
+def test_linear_to_spec():
+    from mpcx import lti, ocp, _lib
+
+    lin = lti.inverted_pendulum_qp()
+    s = ocp.to_spec(lin, max_iter=100, tol=1e-9)
+    assert (s.model, s.nx, s.nu, s.N, s.param_layout) == (_lib.MODEL_LINEAR, 5, 1, 50, _lib.P_X0_STAGEREF)
+    assert (s.lbu[0], s.ubu[0]) == (-200.0, 200.0)
+    assert s.lbx[0] == -1e20 and s.ubx[4] == 1e20
+    assert lin.n_p == 5 + 6 * 50
