@@ -84,7 +84,7 @@ typedef struct mpcx_spec {
   int32_t model;        /* mpcx_model */
   int32_t cost;         /* mpcx_cost */
   int32_t param_layout; /* mpcx_param_layout */
-  int32_t N;            /* horizon (intervals), 1..63 */
+  int32_t N;            /* horizon (intervals), 1..255 (N >= 64: one workgroup of 128/256 lanes per instance) */
   int32_t M;            /* RK4 substeps per interval (M at :101; mpctools M at Trajectory_tracking.py:51) */
   int32_t max_iter;     /* IPOPT max_iter (:190) */
   int32_t device;       /* HIP device ordinal */

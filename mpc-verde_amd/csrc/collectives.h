@@ -51,8 +51,28 @@ struct OpMin {
   __device__ static double f(double a, double b) { return fmin(a, b); }
 };
 
+// Groups wider than a wavefront (G = 128 / 256: horizons N >= 64) span G/64 waves of one
+// workgroup.  Their collectives finish through LDS: every exchange writes the current
+// slot of a 2-slot buffer, passes one workgroup barrier and flips the slot, so the next
+// exchange can never overwrite values a slower wave is still reading (a wave can be at
+// most one barrier ahead).  All waves execute the same sequence of exchanges because
+// every branch around them is group-uniform.
+constexpr int kXchStride = 24;  // doubles per wave per slot (>= NP + NX of the largest model)
+template <int G>
+struct XWave {
+  static constexpr int W = G > 64 ? G / 64 : 1;
+  double* buf;  // [2][W][kXchStride] in LDS (unused when W == 1)
+  int slot;
+  __device__ __forceinline__ double* cur() const { return buf + slot * (W * kXchStride); }
+  __device__ __forceinline__ double* prev() const { return buf + (slot ^ 1) * (W * kXchStride); }
+  __device__ __forceinline__ void sync() {
+    __syncthreads();
+    slot ^= 1;
+  }
+};
+
 template <int G, class Op>
-__device__ __forceinline__ double greduce(double v) {
+__device__ __forceinline__ double greduce(double v, XWave<G>& xw) {
   v = Op::f(v, dpp<kQuadXor1>(v));
   v = Op::f(v, dpp<kQuadXor2>(v));
   v = Op::f(v, dpp<kHalfMirror>(v));
@@ -65,24 +85,56 @@ __device__ __forceinline__ double greduce(double v) {
     const Pair p = halves32(v);
     v = Op::f(p.a, p.b);
   }
+  if constexpr (G > 64) {
+    constexpr int W = G / 64;
+    double* b = xw.cur();
+    if ((threadIdx.x & 63) == 0) b[(threadIdx.x >> 6) * kXchStride] = v;
+    __syncthreads();
+    double r = b[0];
+#pragma unroll
+    for (int w = 1; w < W; ++w) r = Op::f(r, b[w * kXchStride]);  // same order on every wave
+    xw.slot ^= 1;
+    return r;
+  }
   return v;
 }
 template <int G>
-__device__ __forceinline__ double gsum(double v) {
-  return greduce<G, OpSum>(v);
+__device__ __forceinline__ double gsum(double v, XWave<G>& xw) {
+  return greduce<G, OpSum>(v, xw);
 }
 template <int G>
-__device__ __forceinline__ double gmax(double v) {
-  return greduce<G, OpMax>(v);
+__device__ __forceinline__ double gmax(double v, XWave<G>& xw) {
+  return greduce<G, OpMax>(v, xw);
 }
 template <int G>
-__device__ __forceinline__ double gmin(double v) {
-  return greduce<G, OpMin>(v);
+__device__ __forceinline__ double gmin(double v, XWave<G>& xw) {
+  return greduce<G, OpMin>(v, xw);
 }
 // value of lane k+1 / k-1 (whole-wave DPP shift; groups are contiguous and the lanes
 // that would read across a group boundary never use the value)
 __device__ __forceinline__ double from_next(double v) { return dpp<kWaveShl1>(v); }
 __device__ __forceinline__ double from_prev(double v) { return dpp<kWaveShr1>(v); }
+
+// out[i] = v[i] of node k+1 for node-parallel phases; for multi-wave groups lane 63 of
+// wave w receives lane 0 of wave w+1 through LDS.
+template <int G, int n>
+__device__ __forceinline__ void group_next(const double* v, double* out, XWave<G>& xw) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) out[i] = from_next(v[i]);
+  if constexpr (G > 64) {
+    constexpr int W = G / 64;
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    double* b = xw.cur();
+    if (ln == 0 && wv > 0)
+#pragma unroll
+      for (int i = 0; i < n; ++i) b[(wv - 1) * kXchStride + i] = v[i];
+    __syncthreads();
+    if (ln == 63 && wv < W - 1)
+#pragma unroll
+      for (int i = 0; i < n; ++i) out[i] = b[wv * kXchStride + i];
+    xw.slot ^= 1;
+  }
+}
 
 // 1/x to full fp64 accuracy: v_rcp_f64 + two Newton steps (no IEEE division sequence
 // on the sequential critical path)

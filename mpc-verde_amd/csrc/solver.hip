@@ -69,11 +69,15 @@ __device__ __forceinline__ int iuw(int k, int i) {
 }
 
 template <class Model, int G>
-__global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
+__global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2, NP = NX * (NX + 1) / 2;
+  static_assert(NP + NX <= kXchStride && 2 * NX <= kXchStride, "LDS exchange slot too small");
   const int lane = threadIdx.x & 63;
-  const int k = lane & (G - 1);
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = (int)(gid & (G - 1));  // node of this lane
+  // multi-wave groups (G > 64, one workgroup per instance) exchange through LDS
+  __shared__ double xch[2 * XWave<G>::W * kXchStride];
+  XWave<G> xw{xch, 0};
   const int inst = (int)(gid / G);
   const bool valid = inst < a.B;
   const int N = a.N;
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
     hU[i] = own && ub[i] < kInfBound;
     nbnd_l += (int)hL[i] + (int)hU[i];
   }
-  const double nbound = gsum<G>((double)nbnd_l);
+  const double nbound = gsum<G>((double)nbnd_l, xw);
 
   // ---- initial point
   double z[NZ];
@@ -174,11 +178,17 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
   double cdef[NX], c0[NX];  // cdef = F(X_k,U_k) - X_{k+1} (constraint k+1), c0 = x0 - X_0 (lane 0)
   double fs = 1.0;
   auto sweep = [&]() __attribute__((always_inline)) {
-    double ln[NX], xn[NX];
+    double ln[NX], xn[NX], own[2 * NX], nxt[2 * NX];
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
-      ln[i] = from_next(lam[i]);
-      xn[i] = from_next(z[i]);
+      own[i] = lam[i];
+      own[NX + i] = z[i];
+    }
+    group_next<G, 2 * NX>(own, nxt, xw);
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      ln[i] = nxt[i];
+      xn[i] = nxt[NX + i];
     }
     Model::derivs(ma, ctx, z, ln, fs, xf, qv, A, Bm, gq, Hs);
     const double m = hasU ? 1.0 : 0.0;
@@ -203,8 +213,10 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
   int status = valid ? 2 : 0;
   bool done = !valid;
   int it = 0;
-  double dz[NZ], dlam[NX], dzL[NZ], dzU[NZ];
-  double Pk[NP], pk[NX], Kk[NU * NX], kfk[NU];
+  // every per-lane array is defined on every lane (lanes past node N included): no
+  // indeterminate values for the optimiser to exploit
+  double dz[NZ] = {}, dlam[NX] = {}, dzL[NZ] = {}, dzU[NZ] = {};
+  double Pk[NP] = {}, pk[NX] = {}, Kk[NU * NX] = {}, kfk[NU] = {};
 
 #ifdef MPCX_STAMPS
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -222,7 +234,15 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       double gm = 0;
 #pragma unroll
       for (int i = 0; i < NZ; ++i) gm = fmax(gm, fabs(gq[i]));
-      gm = gmax<G>(gm);
+#ifdef MPCX_DEBUG_PRINT
+      const double gm_local = gm;
+#endif
+      gm = gmax<G>(gm, xw);
+#ifdef MPCX_DEBUG_PRINT
+      if (inst == 0 && (k % 32) == 0)
+        printf("k=%d wave=%d gm_local=%g gm=%g slot=%d nbound=%g lds=%p\n", k, (int)(threadIdx.x >> 6), gm_local, gm,
+               xw.slot, nbound, (void*)xw.buf);
+#endif
       fs = gm > 100.0 ? 100.0 / gm : 1.0;
       if (fs != 1.0) {  // group-uniform; given multipliers belong to the unscaled problem
 #pragma unroll
@@ -241,15 +261,14 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       double theta0 = 0;
 #pragma unroll
       for (int i = 0; i < NX; ++i) theta0 += fabs(cdef[i]) + fabs(c0[i]);
-      theta0 = gsum<G>(theta0);
+      theta0 = gsum<G>(theta0, xw);
       theta_max = 1e4 * fmax(1.0, theta0);
       theta_min = 1e-4 * fmax(1.0, theta0);
     }
     STAMP(0);
     // ------------------------------------------------------------ optimality error
     double ln[NX];
-#pragma unroll
-    for (int i = 0; i < NX; ++i) ln[i] = from_next(lam[i]);
+    group_next<G, NX>(lam, ln, xw);
     double Ed = 0, Ecomp0 = 0, Ec = 0, lam1 = 0, z1 = 0;
     double rd[NZ];
 #pragma unroll
@@ -285,11 +304,11 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < NX; ++i) Ec = fmax(Ec, fmax(fabs(cdef[i]), fabs(c0[i])));
-    Ed = gmax<G>(Ed);
-    Ec = gmax<G>(Ec);
-    Ecomp0 = gmax<G>(Ecomp0);
-    lam1 = gsum<G>(lam1);
-    z1 = gsum<G>(z1);
+    Ed = gmax<G>(Ed, xw);
+    Ec = gmax<G>(Ec, xw);
+    Ecomp0 = gmax<G>(Ecomp0, xw);
+    lam1 = gsum<G>(lam1, xw);
+    z1 = gsum<G>(z1, xw);
     const double sd = fmax(kSmax, (lam1 + z1) / (double)(ng + nw)) / kSmax;
     const double sc = fmax(kSmax, nbound > 0 ? z1 / nbound : 0.0) / kSmax;
     const double E0 = fmax(fmax(Ed / sd, Ec), Ecomp0 / sc);
@@ -301,6 +320,10 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       done = true;
       status = 2;
     }
+#ifdef MPCX_DEBUG_PRINT
+    if (inst == 0 && (k % 64) == 0)
+      printf("OPT it=%d k=%d fs=%g Ed=%g Ec=%g E0=%g sd=%g lam1=%g z1=%g\n", it, k, fs, Ed, Ec, E0, sd, lam1, z1);
+#endif
     if (__all(done)) break;
 
     STAMP(1);
@@ -312,7 +335,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
         if (hL[i]) Ecm = fmax(Ecm, fabs((z[i] - lb[i]) * zL[i] - mu));
         if (hU[i]) Ecm = fmax(Ecm, fabs((ub[i] - z[i]) * zU[i] - mu));
       }
-      Ecm = gmax<G>(Ecm);
+      Ecm = gmax<G>(Ecm, xw);
       const double Emu = fmax(fmax(Ed / sd, Ec), Ecm / sc);
       const bool dec = !done && Emu <= kKappaEps * mu && mu > mu_min;
       if (dec) {
@@ -349,7 +372,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
     bool need = !done;  // instance still needs a factorisation
     bool failed = false;
     bool first = true;
-    Fac<NX, NU> fac;
+    Fac<NX, NU> fac = {};
     for (int attempt = 0; attempt < 64; ++attempt) {
       if (!__any(need)) break;
       // node-parallel: stage Hessian + Sigma + delta (off the sequential path)
@@ -370,19 +393,51 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
           p[i] = dl * gp[i];
         }
       }
-      for (int j = N - 1; j >= 0; --j) {
-        double Pin_[NP], pin_[NX];
+      if constexpr (G <= 64) {
+        for (int j = N - 1; j >= 0; --j) {
+          double Pin_[NP], pin_[NX];
 #pragma unroll
-        for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
+          for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
-        if (k == j) okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, Pin_, pin_, P, p, fac);
+          for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
+          if (k == j) okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, Pin_, pin_, P, p, fac);
+        }
+      } else {  // wave by wave, N-side first; the value function crosses waves through LDS
+        const int wv = (int)(threadIdx.x >> 6);
+        for (int ph = XWave<G>::W - 1; ph >= 0; --ph) {
+          if (wv == ph) {
+            const double* in = xw.prev();  // (P, p) of node 64 (ph + 1), written last phase
+            const int jtop = 64 * ph + 63;
+            for (int j = min(N - 1, jtop); j >= 64 * ph; --j) {
+              double Pin_[NP], pin_[NX];
+#pragma unroll
+              for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
+#pragma unroll
+              for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
+              if (j == jtop && lane == 63) {
+#pragma unroll
+                for (int i = 0; i < NP; ++i) Pin_[i] = in[i];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) pin_[i] = in[NP + i];
+              }
+              if (k == j) okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, Pin_, pin_, P, p, fac);
+            }
+            if (ph > 0 && lane == 0) {
+              double* out = xw.cur();
+#pragma unroll
+              for (int i = 0; i < NP; ++i) out[i] = P[i];
+#pragma unroll
+              for (int i = 0; i < NX; ++i) out[NP + i] = p[i];
+            }
+          }
+          xw.sync();
+        }
       }
 #pragma unroll
       for (int i = 0; i < NP; ++i) Pk[i] = P[i];
 #pragma unroll
       for (int i = 0; i < NX; ++i) pk[i] = p[i];
-      const bool ok = gmin<G>(okl ? 1.0 : 0.0) > 0.5;
+      const bool ok = gmin<G>(okl ? 1.0 : 0.0, xw) > 0.5;
       // IPOPT inertia correction (Algorithm IC)
       if (need) {
         if (ok) {
@@ -411,36 +466,61 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       double dxn[NX];
 #pragma unroll
       for (int i = 0; i < NX; ++i) dxn[i] = 0.0;
-      for (int j = 0; j <= N; ++j) {
-        double dxi[NX];
+      auto fwd_node = [&](const double* dxi) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dxi[i] = from_prev(dxn[i]);
-        if (k == j) {
+        for (int i = 0; i < NX; ++i) dz[i] = (k == 0) ? c0[i] : dxi[i];
+        if (k < N) {
 #pragma unroll
-          for (int i = 0; i < NX; ++i) dz[i] = (k == 0) ? c0[i] : dxi[i];
-          if (k < N) {
+          for (int l = 0; l < NU; ++l) {
+            double acc = kfk[l];
 #pragma unroll
-            for (int l = 0; l < NU; ++l) {
-              double acc = kfk[l];
-#pragma unroll
-              for (int m = 0; m < NX; ++m) acc = fma(Kk[l * NX + m], dz[m], acc);
-              dz[NX + l] = acc;
-            }
-#pragma unroll
-            for (int r = 0; r < NX; ++r) {
-              double acc = cdef[r];
-#pragma unroll
-              for (int m = 0; m < NX; ++m)
-                if (Model::AMASK & (1ull << (r * NX + m))) acc = fma(A[r * NX + m], dz[m], acc);
-#pragma unroll
-              for (int l = 0; l < NU; ++l)
-                if (Model::BMASK & (1ull << (r * NU + l))) acc = fma(Bm[r * NU + l], dz[NX + l], acc);
-              dxn[r] = acc;
-            }
-          } else {
-#pragma unroll
-            for (int l = 0; l < NU; ++l) dz[NX + l] = 0.0;
+            for (int m = 0; m < NX; ++m) acc = fma(Kk[l * NX + m], dz[m], acc);
+            dz[NX + l] = acc;
           }
+#pragma unroll
+          for (int r = 0; r < NX; ++r) {
+            double acc = cdef[r];
+#pragma unroll
+            for (int m = 0; m < NX; ++m)
+              if (Model::AMASK & (1ull << (r * NX + m))) acc = fma(A[r * NX + m], dz[m], acc);
+#pragma unroll
+            for (int l = 0; l < NU; ++l)
+              if (Model::BMASK & (1ull << (r * NU + l))) acc = fma(Bm[r * NU + l], dz[NX + l], acc);
+            dxn[r] = acc;
+          }
+        } else {
+#pragma unroll
+          for (int l = 0; l < NU; ++l) dz[NX + l] = 0.0;
+        }
+      };
+      if constexpr (G <= 64) {
+        for (int j = 0; j <= N; ++j) {
+          double dxi[NX];
+#pragma unroll
+          for (int i = 0; i < NX; ++i) dxi[i] = from_prev(dxn[i]);
+          if (k == j) fwd_node(dxi);
+        }
+      } else {  // wave by wave from node 0; the state step crosses waves through LDS
+        const int wv = (int)(threadIdx.x >> 6);
+        for (int ph = 0; ph < XWave<G>::W; ++ph) {
+          if (wv == ph) {
+            const double* in = xw.prev();  // dx of node 64 ph, written by wave ph - 1
+            for (int j = 64 * ph; j <= min(N, 64 * ph + 63); ++j) {
+              double dxi[NX];
+#pragma unroll
+              for (int i = 0; i < NX; ++i) dxi[i] = from_prev(dxn[i]);
+              if (j == 64 * ph && ph > 0 && lane == 0)
+#pragma unroll
+                for (int i = 0; i < NX; ++i) dxi[i] = in[i];
+              if (k == j) fwd_node(dxi);
+            }
+            if (ph < XWave<G>::W - 1 && lane == 63) {
+              double* out = xw.cur();
+#pragma unroll
+              for (int i = 0; i < NX; ++i) out[i] = dxn[i];
+            }
+          }
+          xw.sync();
         }
       }
       // lambda+ = P_k dx_k + p_k (node-parallel, after the sequential sweep)
@@ -483,8 +563,8 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
         gd_l += gp[i] * dz[i];
       }
     }
-    const double amax = gmin<G>(amax_l), az = gmin<G>(az_l), tiny = gmax<G>(tiny_l);
-    const double gd = gsum<G>(gd_l);
+    const double amax = gmin<G>(amax_l, xw), az = gmin<G>(az_l, xw), tiny = gmax<G>(tiny_l, xw);
+    const double gd = gsum<G>(gd_l, xw);
 
     STAMP(6);
     // ------------------------------------------------------------ filter line search
@@ -496,7 +576,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
       if (hL[i]) phk_l -= mu * log(z[i] - lb[i]);
       if (hU[i]) phk_l -= mu * log(ub[i] - z[i]);
     }
-    const double thk = gsum<G>(thk_l), phk = gsum<G>(phk_l);
+    const double thk = gsum<G>(thk_l, xw), phk = gsum<G>(phk_l, xw);
     const bool tinystep = tiny < 10.0 * kEps;
     double alpha = amax;
     bool searching = !done && !tinystep;
@@ -511,8 +591,7 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
 #pragma unroll
       for (int i = 0; i < NZ; ++i) zt[i] = z[i] + alpha * dz[i];
       double xtn[NX];
-#pragma unroll
-      for (int i = 0; i < NX; ++i) xtn[i] = from_next(zt[i]);
+      group_next<G, NX>(zt, xtn, xw);
       double tht_l = 0, pht_l = 0;
       {
         double xft[NX], qt;
@@ -531,9 +610,9 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
         if (hL[i]) pht_l -= mu * log(zt[i] - lb[i]);
         if (hU[i]) pht_l -= mu * log(ub[i] - zt[i]);
       }
-      const double tht = gsum<G>(tht_l), pht = gsum<G>(pht_l);
+      const double tht = gsum<G>(tht_l, xw), pht = gsum<G>(pht_l, xw);
       const double inF = (k < nfilt && tht >= fth && pht >= fph) ? 1.0 : 0.0;
-      const bool infilter = gmax<G>(inF) > 0.5;
+      const bool infilter = gmax<G>(inF, xw) > 0.5;
       if (searching) {
         bool acc = isfinite(pht) && isfinite(tht) && tht <= theta_max && !infilter;
         bool ft = false;
@@ -599,7 +678,11 @@ __global__ __launch_bounds__(64) void solve_kernel(SolveArgs a) {
 #endif
 
   // ---- results
-  const double fsum = gsum<G>(hasU ? qv : 0.0);
+  const double fsum = gsum<G>(hasU ? qv : 0.0, xw);
+#ifdef MPCX_DEBUG_PRINT
+  if (inst == 0 && (k % 64) == 0)
+    printf("END k=%d fs=%g mu=%g it=%d lam0=%g z0=%g zL=%g zU=%g\n", k, fs, mu, it, lam[0], z[0], zL[NX], zU[NX]);
+#endif
   if (valid) {
     double* w = a.w_out + (size_t)inst * nw;
     if (hasX)
@@ -759,12 +842,16 @@ extern "C" int mpcx_diag_set_stamp_buffer(void* d_buf) {
 // ---- launch helpers (called from capi.cpp) -----------------------------------
 template <class Model>
 static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
-  const int G = a.N < 16 ? 16 : (a.N < 32 ? 32 : 64);
+  // lane group: the smallest power of two holding nodes 0..N; G > 64 spans G/64 waves
+  const int G = a.N < 16 ? 16 : a.N < 32 ? 32 : a.N < 64 ? 64 : a.N < 128 ? 128 : 256;
   const long threads = (long)a.B * G;
-  const int blocks = (int)((threads + 63) / 64);
+  const int bs = G > 64 ? G : 64;
+  const int blocks = (int)((threads + bs - 1) / bs);
   if (G == 16) hipLaunchKernelGGL((solve_kernel<Model, 16>), dim3(blocks), dim3(64), 0, stream, a);
   else if (G == 32) hipLaunchKernelGGL((solve_kernel<Model, 32>), dim3(blocks), dim3(64), 0, stream, a);
-  else hipLaunchKernelGGL((solve_kernel<Model, 64>), dim3(blocks), dim3(64), 0, stream, a);
+  else if (G == 64) hipLaunchKernelGGL((solve_kernel<Model, 64>), dim3(blocks), dim3(64), 0, stream, a);
+  else if (G == 128) hipLaunchKernelGGL((solve_kernel<Model, 128>), dim3(blocks), dim3(128), 0, stream, a);
+  else hipLaunchKernelGGL((solve_kernel<Model, 256>), dim3(blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

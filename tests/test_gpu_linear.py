@@ -199,3 +199,27 @@ def test_linear_model_argument_errors(mpcx):
     bad.tab = np.full(50, 7, np.int32)
     with pytest.raises(_lib.MpcxError, match="out of range"):
         h.set_linear_model(bad)
+
+
+@pytest.mark.parametrize("N", [100, 160])
+def test_pendulum_long_horizon_multiwave(mpcx, R, N):
+    """Config 5 family at N = 100 (BASELINE.json) and beyond: one instance spans 2-4
+    wavefronts (128/256-lane groups, LDS handoffs in the Riccati and forward sweeps)."""
+    from mpcx import lti
+
+    lin = lti.inverted_pendulum_qp(N=N)
+    S = mpcx.nlpsol("pend", "mi355x", lin, {"ipopt": {"max_iter": 200}})
+    rng = np.random.default_rng(N)
+    B = 24
+    scale = np.where(np.arange(B) % 3 == 0, 30.0, 1.0)[:, None]
+    x = scale * rng.uniform([-1, -.5, -.2, -.5], [1, .5, .2, .5], size=(B, 4))
+    up = rng.uniform(-50, 50, size=B)
+    r = S.solve_batch(lti.pendulum_params(lin, x, up))
+    assert np.all(r["status"] == 0)
+    A, Bd = R.pendulum_model()
+    for b in range(B):
+        u_ref = R.pendulum_qp_solve(x[b], A, Bd, N=N, uprev=up[b])
+        assert rel(r["w"][b, 5:5 + 6 * 5:6], u_ref) <= U_TOL, b
+    # instances are independent: a ragged sub-batch gives bit-identical results
+    r2 = S.solve_batch(lti.pendulum_params(lin, x[5:12], up[5:12]))
+    np.testing.assert_array_equal(r2["w"], r["w"][5:12])

@@ -221,7 +221,7 @@ def test_empty_batch(mpcx):
     assert r["w"].shape == (0, 53)
 
 
-@pytest.mark.parametrize("N", [1, 2, 15, 16, 31, 32, 50, 63])
+@pytest.mark.parametrize("N", [1, 2, 15, 16, 31, 32, 50, 63, 64, 100, 127, 128, 200, 255])
 def test_horizons(mpcx, C, R, N):
     ocp = mpcx.unicycle_point_to_point(N=N)
     solver = mpcx.nlpsol("s", "mi355x", ocp)
@@ -250,10 +250,11 @@ def test_invalid_arguments(mpcx):
         solver.solve_batch(np.zeros((2, 5)))
     with pytest.raises(ValueError):
         mpcx.nlpsol("s", "ipopt", mpcx.unicycle_point_to_point(N=10))
-    bad = mpcx.unicycle_point_to_point(N=10)
-    bad.N = 0
-    with pytest.raises(mpcx._lib.MpcxError):
-        mpcx.nlpsol("s", "mi355x", bad)
+    for n_bad in (0, 256):
+        bad = mpcx.unicycle_point_to_point(N=10)
+        bad.N = n_bad
+        with pytest.raises(mpcx._lib.MpcxError):
+            mpcx.nlpsol("s", "mi355x", bad)
 
 
 def test_single_shooting_formulation(mpcx, R, golden):
