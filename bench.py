@@ -39,13 +39,36 @@ SWEEP_BYTES_PER_STAGE = 256  # read x_k,u_k,x_{k+1} (64 B) + w
 SWEEP_BYTES_PER_INSTANCE = 48  # P
 
 
+DATA = {
+    2: "synthetic: SURVEY config-2 generator (global instances 0-83 = golden P_j of Casadi/1exemplo.xlsx)",
+    3: "synthetic: SURVEY config-3 generator (phase ~ U[0,20pi), x0 = ref + N(0,0.1^2))",
+    4: "lane_change.csv reference (Trajectory Tracking/), start offsets ~ U{0..449}, x0 = ref + noise",
+    5: "synthetic: x0 ~ U([-1,1]x[-.5,.5]x[-.2,.2]x[-.5,.5]), u_prev = 0",
+}
+DYN = {2: "unicycle", 3: "unicycle", 4: "linear LTV lateral (nx=4, nu=1)", 5: "linear LTI cart-pole (nx=5, nu=1)"}
+
+
+def workload_name(cfg, N):
+    return {
+        2: f"config 2: closed-loop point-to-point MPC, unicycle, multiple shooting N={N}, RK4 M=4 quadrature cost, "
+           "IPOPT tol 1e-8",
+        3: f"config 3: closed-loop circular trajectory tracking (Trajectory_tracking.py), unicycle, multiple "
+           f"shooting N={N}, RK4 M=1 node cost, state bounds, tol 1e-8",
+        4: f"config 4: closed-loop LTV lateral lane-change tracking (Trajectory_tracking_dynamic_model.py), "
+           f"ZOH c2d per step at vref[t], N={N}, |delta|<=20, tol 1e-8",
+        5: f"config 5: closed-loop cart-pole set-point QP (inverted_pendulum_single_shooting_mpctools.py), "
+           f"ZOH c2d T=0.01, move blocking 5 free moves, N={N}, |u|<=200, tol 1e-8",
+    }[cfg]
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
-                    help="2: point-to-point N=20 B=1024 (headline); 3: circular tracking N=30 B=4096")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5),
+                    help="2: point-to-point N=20 B=1024 (headline); 3: circular tracking N=30 B=4096; "
+                         "4: LTV lateral lane change N=50 B=1024/GPU; 5: cart-pole QP N=100 B=2048/GPU")
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU (default per config)")
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--seed", type=int, default=20261015)
@@ -184,9 +207,20 @@ def main():
     from mpcx.device import DeviceLoop
 
     cfg = args.config
-    N = args.N or (20 if cfg == 2 else 30)
-    B = args.batch or (1024 if cfg == 2 else 4096)
-    ocp = mpcx.unicycle_point_to_point(N=N) if cfg == 2 else mpcx.unicycle_tracking(N=N)
+    dev = f"cuda:{local}"
+    N = args.N or {2: 20, 3: 30, 4: 50, 5: 100}[cfg]
+    B = args.batch or {2: 1024, 3: 4096, 4: 1024, 5: 2048}[cfg]
+    start, stop = mdist.shard(B, rank)
+    T_all = args.warmup + args.steps
+    per_step = None  # per-step device updates (stage references / schedules), resident in HBM
+    if cfg in (2, 3):
+        ocp = mpcx.unicycle_point_to_point(N=N) if cfg == 2 else mpcx.unicycle_tracking(N=N)
+    elif cfg == 4:
+        t0, x0, par = mdist.config4_inputs(start, stop, N=N)
+        _, _, vref = mdist.lane_change()
+        ocp = mpcx.lateral_ltv(N=N, Delta=0.05, vref=vref, per_instance_tab=np.minimum(t0, 499))
+    else:
+        ocp = mpcx.inverted_pendulum_qp(N=N)
     solver = mpcx.nlpsol("bench", "mi355x", ocp, {"ipopt": {"max_iter": 3000}}, device=local)
     stream = torch.cuda.current_stream()
 
@@ -196,19 +230,29 @@ def main():
             print(json.dumps({"sweep_ms": ms, "B": args.roofline_batch, "N": N}))
         return
 
-    start, stop = mdist.shard(B, rank)
-    refs = None
     if cfg == 2:
         P0 = mdist.config2_inputs(start, stop, args.seed)
-    else:  # per-step circular references (Trajectory_tracking.py:84-97), precomputed and resident in HBM
+    elif cfg == 3:  # per-step circular references (Trajectory_tracking.py:84-97)
         tau0, P0 = mdist.config3_inputs(start, stop, N=N)
         refs = torch.from_numpy(np.stack([mpcx.ocp.circular_reference(tau0, t, N).reshape(B, -1)
-                                          for t in range(args.warmup + args.steps)])).to(f"cuda:{local}")
-    loop = DeviceLoop(solver, P0, device=f"cuda:{local}", stream=stream)
+                                          for t in range(T_all)])).to(dev)
+        per_step = lambda lp, t: lp.set_stage_refs(refs[t])  # noqa: E731
+    elif cfg == 4:  # instance time t0 + t: references par[t] and the model re-linearised at vref[t] (:117-141)
+        tt = np.minimum(t0[None, :] + np.arange(T_all)[:, None], 499)  # (T_all, B)
+        refs = torch.from_numpy(np.ascontiguousarray(par[tt].reshape(T_all, B, -1))).to(dev)
+        tabs = torch.from_numpy(np.repeat(tt[:, :, None], N, axis=2).astype(np.int32)).to(dev)
+        P0 = ocp.params(x0, par[tt[0]])
+
+        def per_step(lp, t):
+            lp.set_stage_refs(refs[t])
+            lp.set_schedule(tabs[t])
+    else:
+        P0 = mpcx.lti.pendulum_params(ocp, mdist.config5_inputs(start, stop), 0.0)
+    loop = DeviceLoop(solver, P0, device=dev, stream=stream)
 
     for t in range(args.warmup):
-        if refs is not None:
-            loop.set_stage_refs(refs[t])
+        if per_step is not None:
+            per_step(loop, t)
         loop.step()
     torch.cuda.synchronize()
     K = args.steps
@@ -220,8 +264,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(K):
-        if refs is not None:
-            loop.set_stage_refs(refs[args.warmup + i])
+        if per_step is not None:
+            per_step(loop, args.warmup + i)
         ev[i][0].record(stream)
         loop.solve(status_out=status_hist[i], iters_out=iters_hist[i])
         ev[i][1].record(stream)
@@ -238,6 +282,10 @@ def main():
     P_fin = loop.P.cpu().numpy()
     if cfg == 3:  # final error against the stage-0 reference
         P_fin = np.concatenate([P_fin[:, 0:3], P_fin[:, 3:6]], axis=1)
+    elif cfg == 4:  # (y, phi, v_y) against the stage-0 reference
+        P_fin = np.concatenate([P_fin[:, 0:3], P_fin[:, 4:7]], axis=1)
+    elif cfg == 5:  # (x, x', th) against the set point (10, 0, 0)
+        P_fin = np.concatenate([P_fin[:, 0:3], np.tile([ocp.x_target, 0.0, 0.0], (B, 1))], axis=1)
     S = mdist.stats_matrix(P_fin, None, loop.f.cpu().numpy(), status_hist.max(dim=0).values.cpu().numpy(),
                            iters_hist.cpu().numpy())
     S_all = mdist.all_gather_stats(S, device=loop.P.device)
@@ -272,13 +320,9 @@ def main():
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),
             "ms_per_solve_p50": round(p50, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64",
-            "data": ("synthetic: SURVEY config-2 generator (global instances 0-83 = golden P_j of Casadi/1exemplo.xlsx)"
-                     if cfg == 2 else "synthetic: SURVEY config-3 generator (phase ~ U[0,20pi), x0 = ref + N(0,0.1^2))"),
-            "config": {"workload": (f"config 2: closed-loop point-to-point MPC, unicycle, multiple shooting N={N}, "
-                                    "RK4 M=4 quadrature cost, IPOPT tol 1e-8") if cfg == 2 else
-                                   (f"config 3: closed-loop circular trajectory tracking (Trajectory_tracking.py), "
-                                    f"unicycle, multiple shooting N={N}, RK4 M=1 node cost, state bounds, tol 1e-8"),
-                       "dynamics": "unicycle", "N": N, "M": ocp.M, "batch_per_gpu": B, "global_batch": B * world,
+            "data": DATA[cfg],
+            "config": {"workload": workload_name(cfg, N), "dynamics": DYN[cfg], "N": N,
+                       "M": getattr(ocp, "M", None), "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"instance-sharded x{world} (no data-path collective)"},
             "iters_mean": round(float(S_all[:, 1].mean()), 2), "iters_max": int(S_all[:, 2].max()),
             "iters_max_per_step_mean": round(float(iters_max_step), 2),

@@ -120,6 +120,13 @@ const char* mpcx_last_error(void);
 int mpcx_set_linear_model(mpcx_handle* h, int32_t n_tab, const double* A, const double* B, const double* c,
                           const double* W, const int32_t* tab, int32_t tab_rows);
 
+/* Device-resident stage schedule (LTV closed loops: advance the table index of every
+ * instance on the device each step without re-uploading tables).  d_tab is a caller-owned
+ * device array tab_rows x N int32 with the meaning of `tab` above; it must stay valid while
+ * the handle solves.  Indices outside [0, n_tab) are clamped.  d_tab = NULL reverts to the
+ * schedule given to mpcx_set_linear_model (which also clears this one). */
+int mpcx_set_linear_tab_dev(mpcx_handle* h, const int32_t* d_tab, int32_t tab_rows);
+
 /* n_w, n_g, n_p of the NLP described by the handle. */
 int mpcx_dims(const mpcx_handle* h, int32_t* n_w, int32_t* n_g, int32_t* n_p);
 

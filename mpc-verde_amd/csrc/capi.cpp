@@ -34,6 +34,8 @@ struct mpcx_handle {
   double *d_linA = nullptr, *d_linB = nullptr, *d_linc = nullptr, *d_linW = nullptr;
   int32_t* d_lintab = nullptr;
   int lin_ntab = 0, lin_rows = 0;
+  const int32_t* ext_tab = nullptr;  // caller-owned device schedule (mpcx_set_linear_tab_dev)
+  int ext_rows = 0;
 };
 
 namespace {
@@ -272,13 +274,26 @@ int mpcx_set_linear_model(mpcx_handle* h, int32_t n_tab, const double* A, const 
   HIPCHK(hipMemcpy(h->d_lintab, tab, (size_t)tab_rows * N * sizeof(int32_t), hipMemcpyHostToDevice));
   h->lin_ntab = n_tab;
   h->lin_rows = tab_rows;
+  h->ext_tab = nullptr;
+  h->ext_rows = 0;
+  return 0;
+}
+
+int mpcx_set_linear_tab_dev(mpcx_handle* h, const int32_t* d_tab, int32_t tab_rows) {
+  if (!h) return fail(MPCX_EINVAL, "null handle");
+  if (h->spec.model != MPCX_MODEL_LINEAR) return fail(MPCX_EINVAL, "handle is not a linear model");
+  if (!h->d_linA) return fail(MPCX_EINVAL, "linear model tables not set (mpcx_set_linear_model)");
+  if (d_tab && tab_rows < 1) return fail(MPCX_EINVAL, "tab_rows must be >= 1");
+  h->ext_tab = d_tab;
+  h->ext_rows = d_tab ? tab_rows : 0;
   return 0;
 }
 
 static int check_model_ready(const mpcx_handle* h, int B) {
   if (h->spec.model != MPCX_MODEL_LINEAR) return 0;
   if (!h->d_linA) return fail(MPCX_EINVAL, "linear model tables not set (mpcx_set_linear_model)");
-  if (h->lin_rows > 1 && B > h->lin_rows) return fail(MPCX_EINVAL, "batch larger than the per-instance table rows");
+  const int rows = h->ext_tab ? h->ext_rows : h->lin_rows;
+  if (rows > 1 && B > rows) return fail(MPCX_EINVAL, "batch larger than the per-instance table rows");
   return 0;
 }
 
@@ -294,8 +309,8 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
   a.lin.B = h->d_linB;
   a.lin.c = h->d_linc;
   a.lin.W = h->d_linW;
-  a.lin.tab = h->d_lintab;
-  a.lin.per_instance = h->lin_rows > 1 ? 1 : 0;
+  a.lin.tab = h->ext_tab ? h->ext_tab : h->d_lintab;
+  a.lin.per_instance = (h->ext_tab ? h->ext_rows : h->lin_rows) > 1 ? 1 : 0;
   a.lin.n_tab = h->lin_ntab;
   a.N = h->spec.N;
   a.max_iter = h->spec.max_iter;

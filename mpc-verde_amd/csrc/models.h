@@ -64,7 +64,7 @@ struct LinearModel {
   __device__ __forceinline__ static void load_ctx(const ModelArgs& a, int inst, const double* P, int k, bool hasU, Ctx& c) {
     const int N = a.N;
     int j = 0;
-    if (hasU) j = a.lin.tab[(a.lin.per_instance ? (size_t)inst * N : 0) + k];
+    if (hasU) j = min(max(a.lin.tab[(a.lin.per_instance ? (size_t)inst * N : 0) + k], 0), a.lin.n_tab - 1);
     c.A = a.lin.A + (size_t)j * NX * NX;
     c.B = a.lin.B + (size_t)j * NX * NU;
     c.c = a.lin.c + (size_t)j * NX;

@@ -85,6 +85,20 @@ class DeviceLoop:
         with torch.cuda.stream(self.stream):
             self.P[:, self.solver.ocp.nx:].copy_(refs, non_blocking=True)
 
+    def set_schedule(self, tab):
+        """Per-step stage schedule of a linear model: tab is a (B, N) int32 device tensor
+        of table indices read by the next solves/shifts (mpcx_set_linear_tab_dev; LTV
+        re-linearisation per step, Trajectory_tracking_dynamic_model.py:117-141).  The
+        tensor must stay alive while it is in use; None reverts to the uploaded schedule."""
+        lib = _lib.load()
+        if tab is None:
+            _lib.check(lib.mpcx_set_linear_tab_dev(self.solver._h.ptr, None, 0))
+            self._tab = None
+            return
+        assert tab.dtype == torch.int32 and tab.is_contiguous() and tab.shape[0] == self.B
+        self._tab = tab
+        _lib.check(lib.mpcx_set_linear_tab_dev(self.solver._h.ptr, ctypes_void(tab.data_ptr()), self.B))
+
     def step(self):
         self.solve()
         self.shift()

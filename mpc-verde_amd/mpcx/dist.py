@@ -87,6 +87,45 @@ def config3_inputs(start: int, stop: int, N: int = 30, seed: int = 20261016):
     return tau0, P
 
 
+def lane_change(path=None):
+    """Trajectory Tracking/lane_change.csv (x, y, uref; 500 rows), shipped as tests/golden/lane_change.csv."""
+    import csv
+
+    if path is None:
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        path = os.path.join(root, "tests", "golden", "lane_change.csv")
+    with open(path) as f:
+        rows = [tuple(float(v) for v in r.values()) for r in csv.DictReader(f)]
+    return tuple(np.array(c) for c in zip(*rows))
+
+
+def config4_inputs(start: int, stop: int, N: int = 50, seed: int = 20261017):
+    """SURVEY.md §8(d) config 4 (LTV lateral model, lane_change.csv): start offset
+    t0 ~ U{0..449}; x0 = (y_ref, phi_ref, v_ref, r_ref)(t0) + N(0, diag(.1, .02, .1, .02)^2).
+    Returns (t0 (n,) int, x0 (n, 4), par (500, N, 5) per-time stage references)."""
+    from .lti import lateral_references
+
+    xr, yr, vr = lane_change()
+    par = lateral_references(xr, yr, vr, Delta=0.05, horizon=N)
+    n = stop - start
+    t0 = np.zeros(n, np.int64)
+    x0 = np.zeros((n, 4))
+    for i, g in enumerate(range(start, stop)):
+        rng = np.random.default_rng([seed, g])
+        t0[i] = rng.integers(0, 450)
+        x0[i] = par[t0[i], 0, 0:4] + rng.normal(scale=[0.1, 0.02, 0.1, 0.02])
+    return t0, x0, par
+
+
+def config5_inputs(start: int, stop: int, seed: int = 20261018):
+    """SURVEY.md §8(d) config 5 (cart-pole QP): x0 ~ U([-1,1]x[-.5,.5]x[-.2,.2]x[-.5,.5]), u_prev = 0."""
+    n = stop - start
+    x0 = np.zeros((n, 4))
+    for i, g in enumerate(range(start, stop)):
+        x0[i] = np.random.default_rng([seed, g]).uniform([-1, -.5, -.2, -.5], [1, .5, .2, .5])
+    return x0
+
+
 def stats_matrix(P, w, f, status, iters_hist):
     """Per-instance closed-loop statistics, (B, len(STAT_FIELDS)) float64."""
     B = P.shape[0]

@@ -92,3 +92,17 @@ def test_world_size_2_gloo_matches_single_process():
     Pf, res, iters = _closed_loop_shard(P, steps, N)
     S_ref = dist.stats_matrix(Pf, res["w"], res["f"], res["status"], iters)
     assert np.array_equal(S_all, S_ref)  # independent instances: bitwise identical
+
+
+def test_config4_config5_inputs_shard_invariant():
+    from mpcx import dist as mdist
+
+    t0a, x0a, par = mdist.config4_inputs(0, 64, N=10)
+    t0b, x0b, _ = mdist.config4_inputs(32, 64, N=10)
+    np.testing.assert_array_equal(t0a[32:], t0b)
+    np.testing.assert_array_equal(x0a[32:], x0b)
+    assert t0a.min() >= 0 and t0a.max() <= 449 and par.shape == (500, 10, 5)
+    a = mdist.config5_inputs(0, 40)
+    b = mdist.config5_inputs(10, 40)
+    np.testing.assert_array_equal(a[10:], b)
+    assert np.all(np.abs(a) <= [1, .5, .2, .5])

@@ -223,3 +223,39 @@ def test_pendulum_long_horizon_multiwave(mpcx, R, N):
     # instances are independent: a ragged sub-batch gives bit-identical results
     r2 = S.solve_batch(lti.pendulum_params(lin, x[5:12], up[5:12]))
     np.testing.assert_array_equal(r2["w"], r["w"][5:12])
+
+
+def test_ltv_device_loop_with_device_schedule(mpcx, R):
+    """Config-4 closed loop on the device: per step the stage references and the per-instance
+    schedule (model re-linearised at vref[t], mpcx_set_linear_tab_dev) advance; compared with
+    a host loop of exact LQ solves using the same tables."""
+    import torch
+    from mpcx import dist as mdist
+    from mpcx.device import DeviceLoop
+
+    N, B, T = 20, 16, 6
+    t0, x0, par = mdist.config4_inputs(0, B, N=N)
+    _, _, vref = mdist.lane_change()
+    lin = mpcx.lateral_ltv(N=N, Delta=0.05, vref=vref, per_instance_tab=t0)
+    S = mpcx.nlpsol("ltv", "mi355x", lin, {"ipopt": {"max_iter": 300}})
+    tt = np.minimum(t0[None, :] + np.arange(T)[:, None], 499)
+    refs = torch.from_numpy(np.ascontiguousarray(par[tt].reshape(T, B, -1))).to("cuda:0")
+    tabs = torch.from_numpy(np.repeat(tt[:, :, None], N, axis=2).astype(np.int32)).to("cuda:0")
+    loop = DeviceLoop(S, lin.params(x0, par[tt[0]]), device="cuda:0")
+    x = x0.copy()
+    for t in range(T):
+        loop.set_stage_refs(refs[t])
+        loop.set_schedule(tabs[t])
+        loop.step()
+        torch.cuda.synchronize()
+        assert np.all(loop.status.cpu().numpy() == 0)
+        w = loop.w.cpu().numpy()
+        u0 = np.empty(B)
+        for b in range(B):
+            j = tt[t, b]
+            _, U_ref, _ = R.lq_solve(x[b], lin.A, lin.B, lin.c, lin.W, np.full(N, j), par[j], [-20], [20])
+            assert rel(w[b, 4:4 + 5 * N:5], U_ref[:, 0]) <= U_TOL, (t, b)
+            u0[b] = w[b, 4]
+            x[b] = lin.A[j] @ x[b] + lin.B[j][:, 0] * u0[b]
+        np.testing.assert_allclose(loop.P.cpu().numpy()[:, 0:4], x, rtol=1e-12, atol=1e-12)
+    loop.set_schedule(None)
