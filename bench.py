@@ -267,9 +267,8 @@ def main():
         if per_step is not None:
             per_step(loop, args.warmup + i)
         ev[i][0].record(stream)
-        loop.solve(status_out=status_hist[i], iters_out=iters_hist[i])
+        loop.step(status_out=status_hist[i], iters_out=iters_hist[i])  # solve + plant/shift, one launch
         ev[i][1].record(stream)
-        loop.shift()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:

@@ -173,6 +173,21 @@ int mpcx_shift_dev(mpcx_handle* h, int32_t B, double* d_P, const double* d_w, do
                    const double* d_lam_g, double* d_lam_g0_next, const double* d_lam_x, double* d_lam_x0_next,
                    void* stream);
 
+/* One closed-loop step on the device in ONE kernel launch: the batched solve of
+ * mpcx_solve_batch_dev followed, in the same kernel, by the receding-horizon update of
+ * mpcx_shift_dev (identical results), written IN PLACE:
+ *   d_P[:, 0:nx]  <- F(x0, u_0*)                      (plant, :273)
+ *   d_w0          <- solution shifted by one interval  (warm start of the next step)
+ *   d_lam_g0/d_lam_x0 <- multipliers shifted alike (may be NULL: not kept)
+ * flags: MPCX_STEP_COLD -- ignore d_w0 / multipliers on input (cold start, :212-213);
+ *        MPCX_STEP_PRIMAL_ONLY -- warm primal start, default multiplier initialisation.
+ * Otherwise the solve starts from d_w0 and (if given) the shifted multipliers as IPOPT's
+ * warm_start_init_point.  Solution outputs as in mpcx_solve_batch_dev (d_w_out required). */
+enum mpcx_step_flags { MPCX_STEP_COLD = 1, MPCX_STEP_PRIMAL_ONLY = 2 };
+int mpcx_step_dev(mpcx_handle* h, int32_t B, double* d_P, double* d_w0, double* d_lam_g0, double* d_lam_x0,
+                  int32_t flags, double* d_w_out, double* d_f_out, double* d_lam_g, double* d_lam_x,
+                  int32_t* d_status, int32_t* d_iters, void* stream);
+
 /* RK4 + Jacobian sweep over B x N shooting intervals (host pointers).
  *   w      B x n_w decision vectors (interleaved layout)
  *   P      B x n_p parameters

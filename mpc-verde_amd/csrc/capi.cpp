@@ -300,7 +300,7 @@ static int check_model_ready(const mpcx_handle* h, int B) {
 static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, const double* w0, const double* lam0,
                                  const double* lamx0, const double* lbw, const double* ubw, double* w, double* f,
                                  double* lam, double* lamx, int32_t* st, int32_t* it) {
-  mpcx::SolveArgs a;
+  mpcx::SolveArgs a{};
   a.B = B;
   a.model = h->spec.model;
   a.nx = h->spec.nx;
@@ -347,6 +347,28 @@ int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const dou
   HIPCHK(hipSetDevice(h->spec.device));
   mpcx::SolveArgs a = make_args(h, B, d_P, d_w0, d_lam_g0, d_lam_x0, h->d_lbw, h->d_ubw, d_w_out, d_f_out, d_lam_g,
                                 d_lam_x, d_status, d_iters);
+  HIPCHK(mpcx::launch_solve(a, (hipStream_t)stream));
+  return 0;
+}
+
+int mpcx_step_dev(mpcx_handle* h, int32_t B, double* d_P, double* d_w0, double* d_lam_g0, double* d_lam_x0,
+                  int32_t flags, double* d_w_out, double* d_f_out, double* d_lam_g, double* d_lam_x,
+                  int32_t* d_status, int32_t* d_iters, void* stream) {
+  if (!h || !d_P || !d_w0 || !d_w_out) return fail(MPCX_EINVAL, "null argument");
+  if (B < 0) return fail(MPCX_EINVAL, "B < 0");
+  if (flags & ~(MPCX_STEP_COLD | MPCX_STEP_PRIMAL_ONLY)) return fail(MPCX_EINVAL, "unknown flags");
+  if (B == 0) return 0;
+  if (int r = check_model_ready(h, B)) return r;
+  HIPCHK(hipSetDevice(h->spec.device));
+  const bool cold = flags & MPCX_STEP_COLD;
+  const bool duals = !cold && !(flags & MPCX_STEP_PRIMAL_ONLY);
+  mpcx::SolveArgs a = make_args(h, B, d_P, cold ? nullptr : d_w0, duals ? d_lam_g0 : nullptr,
+                                duals ? d_lam_x0 : nullptr, h->d_lbw, h->d_ubw, d_w_out, d_f_out, d_lam_g, d_lam_x,
+                                d_status, d_iters);
+  a.P_next = d_P;
+  a.w0_next = d_w0;
+  a.lam0_next = d_lam_g0;
+  a.lamx0_next = d_lam_x0;
   HIPCHK(mpcx::launch_solve(a, (hipStream_t)stream));
   return 0;
 }

@@ -39,6 +39,12 @@ struct SolveArgs {
   double* lamx_out;     // B x nw or null
   int32_t* status;      // B or null
   int32_t* iters;       // B or null
+  // fused receding-horizon update (mpcx_step_dev): written after the solve, in place
+  // allowed (every slot is read and written by the same lane).  Null = no update.
+  double* P_next;       // B x p_stride: x0 <- F(x0, u_0*)
+  double* w0_next;      // B x nw: solution shifted one interval
+  double* lam0_next;    // B x ng or null
+  double* lamx0_next;   // B x nw or null
 };
 
 // What a stage model reads (a local copy: taking the address of the kernel argument

@@ -71,7 +71,7 @@ __device__ __forceinline__ int iuw(int k, int i) {
 template <class Model, int G>
 __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2, NP = NX * (NX + 1) / 2;
-  static_assert(NP + NX <= kXchStride && 2 * NX <= kXchStride, "LDS exchange slot too small");
+  static_assert(NP + NX <= kXchStride && 2 * NZ + NX <= kXchStride, "LDS exchange slot too small");
   const int lane = threadIdx.x & 63;
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int k = (int)(gid & (G - 1));  // node of this lane
@@ -702,6 +702,51 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
       if (a.f_out) a.f_out[inst] = fsum;
       if (a.status) a.status[inst] = status;
       if (a.iters) a.iters[inst] = it > a.max_iter ? a.max_iter : it;
+    }
+  }
+
+  // ---- fused receding-horizon update (Casadi/multiple_shooting_casadi.py:271-287), the
+  //      same result as shift_kernel: node k takes node k+1's primal and multipliers
+  //      (last node / interval repeated), x0 <- F(x0, u_0*) on lane 0.
+  if (a.w0_next) {  // kernel-uniform
+    constexpr int NS = NZ + NX + NZ;  // z, lam, lamx of the next node
+    double own[NS], nxt[NS];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+      own[i] = z[i];
+      own[NZ + NX + i] = (zU[i] - zL[i]) / fs;
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) own[NZ + i] = lam[i] / fs;
+    group_next<G, NS>(own, nxt, xw);
+    if (valid) {
+      const bool lastX = (k == N), lastU = (k == N - 1);
+      double* w0n = a.w0_next + (size_t)inst * nw;
+      if (hasX)
+        for (int i = 0; i < NX; ++i) w0n[ixw<NX, NU>(k, i)] = lastX ? own[i] : nxt[i];
+      if (hasU)
+        for (int i = 0; i < NU; ++i) w0n[iuw<NX, NU>(k, i)] = lastU ? own[NX + i] : nxt[NX + i];
+      if (a.lam0_next && hasX)
+        for (int i = 0; i < NX; ++i) a.lam0_next[(size_t)inst * ng + NX * k + i] = lastX ? own[NZ + i] : nxt[NZ + i];
+      if (a.lamx0_next) {
+        double* lx = a.lamx0_next + (size_t)inst * nw;
+        if (hasX)
+          for (int i = 0; i < NX; ++i)
+            lx[ixw<NX, NU>(k, i)] = k == 0 ? 0.0 : (lastX ? own[NZ + NX + i] : nxt[NZ + NX + i]);
+        if (hasU)
+          for (int i = 0; i < NU; ++i)
+            lx[iuw<NX, NU>(k, i)] = lastU ? own[NZ + NX + NX + i] : nxt[NZ + NX + NX + i];
+      }
+      if (k == 0) {  // plant: x0 <- F(x0, u_0*) with the stage-0 model
+        double zp[NZ], xfp[NX], qp;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) zp[i] = x0[i];
+#pragma unroll
+        for (int i = 0; i < NU; ++i) zp[NX + i] = z[NX + i];
+        Model::value(ma, ctx, zp, xfp, qp);
+        double* pn = a.P_next + (size_t)inst * a.p_stride;
+        for (int i = 0; i < NX; ++i) pn[i] = xfp[i];
+      }
     }
   }
 }

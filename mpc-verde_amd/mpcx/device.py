@@ -32,8 +32,8 @@ class DeviceLoop:
     and w0 the shifted warm start.  With warm_duals (default) the constraint and
     bound multipliers are shifted as well and the next solve starts as IPOPT's
     warm_start_init_point (spec.warm_*); the first solve is always cold.
-    ``step()`` enqueues a solve and the plant/shift update on ``stream`` and
-    returns immediately.
+    ``step()`` enqueues one fused solve + plant/shift launch on ``stream`` and
+    returns immediately (``solve()`` / ``shift()`` do the two halves separately).
     """
 
     def __init__(self, solver: Solver, P0, device="cuda", stream=None, cold_first=True, warm_duals=True):
@@ -99,6 +99,18 @@ class DeviceLoop:
         self._tab = tab
         _lib.check(lib.mpcx_set_linear_tab_dev(self.solver._h.ptr, ctypes_void(tab.data_ptr()), self.B))
 
-    def step(self):
-        self.solve()
-        self.shift()
+    def step(self, status_out=None, iters_out=None):
+        """One closed-loop step = ONE kernel launch (mpcx_step_dev): the batched solve and,
+        fused into its epilogue, the plant + shifted warm start (same result as
+        solve() followed by shift())."""
+        lib = _lib.load()
+        s = ctypes_void(self.stream.cuda_stream)
+        flags = _lib.STEP_COLD if self._cold else (0 if self.warm_duals else _lib.STEP_PRIMAL_ONLY)
+        d = self.warm_duals
+        st = self.status if status_out is None else status_out
+        it = self.iters if iters_out is None else iters_out
+        _lib.check(lib.mpcx_step_dev(self.solver._h.ptr, self.B, _ptr(self.P), _ptr(self.w0),
+                                     _ptr(self.lam0) if d else None, _ptr(self.lamx0) if d else None, flags,
+                                     _ptr(self.w), _ptr(self.f), _ptr(self.lam), _ptr(self.lamx), _ptr(st), _ptr(it),
+                                     s))
+        self._cold = False

@@ -408,3 +408,25 @@ def solver_bounds(ocp):
 
     lb, ub = nlp_ref.ms_bounds(nlp_ref.tracking_ocp(N=ocp.N))
     return lb, ub
+
+
+@pytest.mark.parametrize("N,B", [(20, 200), (100, 24)])
+def test_fused_step_matches_solve_then_shift(mpcx, N, B):
+    """mpcx_step_dev (solve + plant/shift fused in one kernel, updated in place) gives
+    bit-identical P, warm start and multipliers to mpcx_solve_batch_dev + mpcx_shift_dev,
+    over several closed-loop steps (N = 100: multi-wave groups, LDS handoff of node k+1)."""
+    import torch
+    from mpcx import dist
+    from mpcx.device import DeviceLoop
+
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=N))
+    P0 = dist.config2_inputs(0, B)
+    fused, split = DeviceLoop(solver, P0), DeviceLoop(solver, P0)
+    for _ in range(4):
+        fused.step()
+        split.solve()
+        split.shift()
+        torch.cuda.synchronize()
+        for name in ("P", "w", "w0", "lam", "lam0", "lamx", "lamx0", "f", "status", "iters"):
+            a, b = getattr(fused, name).cpu().numpy(), getattr(split, name).cpu().numpy()
+            np.testing.assert_array_equal(a, b, err_msg=name)

@@ -20,7 +20,7 @@ import sys
 
 
 def values(d, counter):
-    f = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
+    f = sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True))[0]
     return [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
             if "rk4_sens" in r["Kernel_Name"] and r["Counter_Name"] == counter]
 
