@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--roofline-reps", type=int, default=20)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum timed CPU-baseline solve time")
     ap.add_argument("--profile-sweep-only", action="store_true", help="only launch the sweep (for rocprofv3 --pmc)")
     return ap.parse_args()
 
@@ -106,34 +106,40 @@ def shift_lamx_np(lamx, N):
     return out
 
 
-def cpu_baseline(P0, N, steps, cores, warm=(1e-4, 1e-4, 1e-4)):
-    """C++ oracle (port of the same NLP + IPOPT-style IPM) on host cores: `steps`
-    closed-loop steps of the same instances with the same warm start as the GPU
-    loop (first step cold, then shifted primal + multipliers), solve calls timed."""
+def cpu_baseline(make_P, N, steps, cores, min_seconds=10.0, max_reps=64, warm=(1e-4, 1e-4, 1e-4)):
+    """C++ oracle (port of the same NLP + IPOPT-style IPM) on host cores: closed loops of
+    `steps` steps with the same warm start as the GPU loop (first step cold, then shifted
+    primal + multipliers), solve calls timed.  Repeated on fresh instance blocks
+    (make_P(rep) -> (B, 6)) until >= min_seconds of solve time (a bounded sample)."""
     from oracle import ipm_ref, nlp_ref
 
     ipm_ref.build()
     ocp = nlp_ref.UnicycleOCP(N=N)
-    P = P0.copy()
-    B = P.shape[0]
-    w0 = _cold(P, N, nlp_ref)
-    lam0 = lamx0 = None
     t_solve = 0.0
-    for s in range(steps):
-        t0 = time.perf_counter()
-        if s == 0:
-            r = ipm_ref.solve_batch(ocp, P, w0=w0, nthreads=cores)
-            r["lam_x"] = np.zeros_like(r["w"])
-        else:
-            r = ipm_ref.solve_batch_warm(ocp, P, w0, lam0=lam0, lamx0=lamx0, mu_init=warm[0], bound_push=warm[1],
-                                         mult_push=warm[2], nthreads=cores)
-        t_solve += time.perf_counter() - t0
-        xf, _ = nlp_ref.F(P[:, 0:3], r["w"][:, 3:5], P[:, 3:6], ocp)
-        P[:, 0:3] = xf
-        w0 = shift_np(r["w"], N)
-        lam0 = shift_lam_np(r["lam_g"], N)
-        lamx0 = shift_lamx_np(r["lam_x"], N)
-    return B * steps / t_solve, t_solve
+    n = 0
+    reps = 0
+    while reps < max_reps and (reps == 0 or t_solve < min_seconds):
+        P = make_P(reps).copy()
+        B = P.shape[0]
+        w0 = _cold(P, N, nlp_ref)
+        lam0 = lamx0 = None
+        for s in range(steps):
+            t0 = time.perf_counter()
+            if s == 0:
+                r = ipm_ref.solve_batch(ocp, P, w0=w0, nthreads=cores)
+                r["lam_x"] = np.zeros_like(r["w"])
+            else:
+                r = ipm_ref.solve_batch_warm(ocp, P, w0, lam0=lam0, lamx0=lamx0, mu_init=warm[0],
+                                             bound_push=warm[1], mult_push=warm[2], nthreads=cores)
+            t_solve += time.perf_counter() - t0
+            n += B
+            xf, _ = nlp_ref.F(P[:, 0:3], r["w"][:, 3:5], P[:, 3:6], ocp)
+            P[:, 0:3] = xf
+            w0 = shift_np(r["w"], N)
+            lam0 = shift_lam_np(r["lam_g"], N)
+            lamx0 = shift_lamx_np(r["lam_x"], N)
+        reps += 1
+    return n / t_solve, t_solve, reps
 
 
 def _cold(P, N, nlp_ref):
@@ -307,10 +313,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu and cfg == 2:
         cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
         cores = max(1, min(cores, os.cpu_count() or 1))
-        rate, t = cpu_baseline(P0, N, args.cpu_steps, cores)
+        rate, t, reps = cpu_baseline(lambda r: mdist.config2_inputs(r * B, (r + 1) * B, args.seed), N,
+                                     args.warmup + args.steps, cores, min_seconds=args.cpu_seconds)
         cpu = {"value": round(rate, 1), "unit": "solves/s", "cores": cores, "kind": "port",
-               "sample": f"{args.cpu_steps} closed-loop steps x {B} config-2 instances (N={N}), solve calls timed, "
-                         f"{t:.1f} s wall"}
+               "sample": f"{reps} x ({args.warmup + args.steps}-step closed loop of {B} config-2 instances, "
+                         f"N={N}, same warm start as the GPU loop); {t:.1f} s of timed solve calls on {cores} "
+                         "OpenMP threads"}
 
     if rank == 0:
         total = world * B * K

@@ -430,3 +430,23 @@ def test_fused_step_matches_solve_then_shift(mpcx, N, B):
         for name in ("P", "w", "w0", "lam", "lam0", "lamx", "lamx0", "f", "status", "iters"):
             a, b = getattr(fused, name).cpu().numpy(), getattr(split, name).cpu().numpy()
             np.testing.assert_array_equal(a, b, err_msg=name)
+
+
+def test_integration_stub_runs():
+    """INTEGRATION.md §5 (the raw ctypes binding a maintainer would add) runs verbatim in a
+    fresh process and prints the golden u0* = (1, pi/4)."""
+    import os
+    import re
+    import subprocess
+    import sys
+
+    from conftest import ROOT, PKG
+
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = text[text.index("## 5."):]
+    code = re.search(r"```python\n(.*?)```", sec, re.S).group(1)
+    env = dict(os.environ, MPCX_LIB=os.path.join(PKG, "mpcx", "libmpcx.so"))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    u = [float(v) for v in out.stdout.strip().strip("[]").split()]
+    assert abs(u[0] - 1.0) < 1e-6 and abs(u[1] - math.pi / 4) < 1e-6
