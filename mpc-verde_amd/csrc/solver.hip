@@ -68,6 +68,26 @@ __device__ __forceinline__ int iuw(int k, int i) {
   return NX + (NX + NU) * k + i;
 }
 
+// sum of log(slack) over the bounded components of a lane's variables as ONE log: the
+// product of the slacks' frexp mantissas (each in [0.5, 1), at most 2 NZ factors, so no
+// under/overflow) plus the exponents times ln 2.  One log instead of one per bound.
+template <int NZ>
+__device__ __forceinline__ double barrier_logsum(const double* z, const double* lb, const double* ub, const bool* hL,
+                                                 const bool* hU) {
+  double m = 1.0;
+  int e = 0;
+#pragma unroll
+  for (int i = 0; i < NZ; ++i) {
+    int el, eu;
+    const double ml = frexp(z[i] - lb[i], &el), mu = frexp(ub[i] - z[i], &eu);
+    m *= hL[i] ? ml : 1.0;
+    e += hL[i] ? el : 0;
+    m *= hU[i] ? mu : 1.0;
+    e += hU[i] ? eu : 0;
+  }
+  return log(m) + (double)e * 0.69314718055994530942;
+}
+
 template <class Model, int G>
 __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2, NP = NX * (NX + 1) / 2;
@@ -339,7 +359,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
       const double Emu = fmax(fmax(Ed / sd, Ec), Ecm / sc);
       const bool dec = !done && Emu <= kKappaEps * mu && mu > mu_min;
       if (dec) {
-        mu = fmax(mu_min, fmin(kKappaMu * mu, pow(mu, kThetaMu)));
+        static_assert(kThetaMu == 1.5, "mu^theta_mu evaluated as mu * sqrt(mu)");
+        mu = fmax(mu_min, fmin(kKappaMu * mu, mu * sqrt(mu)));
         tau = fmax(kTauMin, 1.0 - mu);
         nfilt = 0;
         fnext = 0;
@@ -568,22 +589,18 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
 
     STAMP(6);
     // ------------------------------------------------------------ filter line search
-    double thk_l = 0, phk_l = hasU ? fs * qv : 0.0;
+    double thk_l = 0, phk_l = (hasU ? fs * qv : 0.0) - mu * barrier_logsum<NZ>(z, lb, ub, hL, hU);
 #pragma unroll
     for (int i = 0; i < NX; ++i) thk_l += fabs(cdef[i]) + fabs(c0[i]);
-#pragma unroll
-    for (int i = 0; i < NZ; ++i) {
-      if (hL[i]) phk_l -= mu * log(z[i] - lb[i]);
-      if (hU[i]) phk_l -= mu * log(ub[i] - z[i]);
-    }
     const double thk = gsum<G>(thk_l, xw), phk = gsum<G>(phk_l, xw);
     const bool tinystep = tiny < 10.0 * kEps;
     double alpha = amax;
     bool searching = !done && !tinystep;
     bool accepted = !done && tinystep;
     bool ftype = tinystep;
-    const double amin = gd < 0 ? kGammaAlpha * fmin(kGammaTheta, fmin(kGammaPhi * thk / (-gd),
-                                                                       kDeltaSw * pow(thk, kSTheta) / pow(-gd, kSPhi)))
+    // switching-condition powers, loop-invariant over the trials
+    const double pw_th = pow(thk, kSTheta), pw_gd = gd < 0 ? pow(-gd, kSPhi) : 0.0;
+    const double amin = gd < 0 ? kGammaAlpha * fmin(kGammaTheta, fmin(kGammaPhi * thk / (-gd), kDeltaSw * pw_th / pw_gd))
                                : kGammaAlpha * kGammaTheta;
     for (int ls = 0; ls < 80; ++ls) {
       if (!__any(searching)) break;
@@ -605,11 +622,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
       if (valid && k == 0)
 #pragma unroll
         for (int i = 0; i < NX; ++i) tht_l += fabs(x0[i] - zt[i]);
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) {
-        if (hL[i]) pht_l -= mu * log(zt[i] - lb[i]);
-        if (hU[i]) pht_l -= mu * log(ub[i] - zt[i]);
-      }
+      pht_l -= mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU);
       const double tht = gsum<G>(tht_l, xw), pht = gsum<G>(pht_l, xw);
       const double inF = (k < nfilt && tht >= fth && pht >= fph) ? 1.0 : 0.0;
       const bool infilter = gmax<G>(inF, xw) > 0.5;
@@ -617,7 +630,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
         bool acc = isfinite(pht) && isfinite(tht) && tht <= theta_max && !infilter;
         bool ft = false;
         if (acc) {
-          const bool sw = gd < 0 && alpha * pow(-gd, kSPhi) > kDeltaSw * pow(thk, kSTheta);
+          const bool sw = gd < 0 && alpha * pw_gd > kDeltaSw * pw_th;
           if (thk <= theta_min && sw) {
             acc = pht - phk <= kEtaPhi * alpha * gd + 10.0 * kEps * fabs(phk);
             ft = acc;
