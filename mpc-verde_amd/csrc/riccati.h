@@ -34,24 +34,34 @@ __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp,
   constexpr int NZ = NX + NU;
   static_assert(NU == 1 || NU == 2, "NU must be 1 or 2");
   auto Pm = [&](int i, int j) { return P[symix(i, j, NX)]; };
-  // PA = P A, PB = P B
+  // PA = P A, PB = P B.  Sums start from their first structural term (a product, not an
+  // fma into 0.0): a model's structural ones then fold away (P * 1.0 == P exactly, while
+  // fma(P, 1.0, 0.0) must be kept for the sign of zero).
   double PA[NX * NX], PB[NX * NU];
 #pragma unroll
   for (int r = 0; r < NX; ++r) {
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       double acc = 0.0;
+      bool first = true;
 #pragma unroll
       for (int m = 0; m < NX; ++m)
-        if (AMASK & (1ull << (m * NX + j))) acc = fma(Pm(r, m), A[m * NX + j], acc);
+        if (AMASK & (1ull << (m * NX + j))) {
+          acc = first ? Pm(r, m) * A[m * NX + j] : fma(Pm(r, m), A[m * NX + j], acc);
+          first = false;
+        }
       PA[r * NX + j] = acc;
     }
 #pragma unroll
     for (int l = 0; l < NU; ++l) {
       double acc = 0.0;
+      bool first = true;
 #pragma unroll
       for (int m = 0; m < NX; ++m)
-        if (BMASK & (1ull << (m * NU + l))) acc = fma(Pm(r, m), Bm[m * NU + l], acc);
+        if (BMASK & (1ull << (m * NU + l))) {
+          acc = first ? Pm(r, m) * Bm[m * NU + l] : fma(Pm(r, m), Bm[m * NU + l], acc);
+          first = false;
+        }
       PB[r * NU + l] = acc;
     }
   }

@@ -487,31 +487,34 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
       double dxn[NX];
 #pragma unroll
       for (int i = 0; i < NX; ++i) dxn[i] = 0.0;
+      // closed-loop map of the step, node-parallel (off the sequential chain):
+      // dx_{k+1} = (A + B K) dx_k + (c + B k_f);  du_k = k_f + K dx_k afterwards
+      double Acl[NX * NX], ccl[NX];
+#pragma unroll
+      for (int r = 0; r < NX; ++r) {
+        double acc = cdef[r];
+#pragma unroll
+        for (int l = 0; l < NU; ++l)
+          if (Model::BMASK & (1ull << (r * NU + l))) acc = fma(Bm[r * NU + l], kfk[l], acc);
+        ccl[r] = acc;
+#pragma unroll
+        for (int m = 0; m < NX; ++m) {
+          double e = (Model::AMASK & (1ull << (r * NX + m))) ? A[r * NX + m] : 0.0;
+#pragma unroll
+          for (int l = 0; l < NU; ++l)
+            if (Model::BMASK & (1ull << (r * NU + l))) e = fma(Bm[r * NU + l], Kk[l * NX + m], e);
+          Acl[r * NX + m] = e;
+        }
+      }
       auto fwd_node = [&](const double* dxi) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) dz[i] = (k == 0) ? c0[i] : dxi[i];
-        if (k < N) {
 #pragma unroll
-          for (int l = 0; l < NU; ++l) {
-            double acc = kfk[l];
+        for (int r = 0; r < NX; ++r) {
+          double acc = ccl[r];
 #pragma unroll
-            for (int m = 0; m < NX; ++m) acc = fma(Kk[l * NX + m], dz[m], acc);
-            dz[NX + l] = acc;
-          }
-#pragma unroll
-          for (int r = 0; r < NX; ++r) {
-            double acc = cdef[r];
-#pragma unroll
-            for (int m = 0; m < NX; ++m)
-              if (Model::AMASK & (1ull << (r * NX + m))) acc = fma(A[r * NX + m], dz[m], acc);
-#pragma unroll
-            for (int l = 0; l < NU; ++l)
-              if (Model::BMASK & (1ull << (r * NU + l))) acc = fma(Bm[r * NU + l], dz[NX + l], acc);
-            dxn[r] = acc;
-          }
-        } else {
-#pragma unroll
-          for (int l = 0; l < NU; ++l) dz[NX + l] = 0.0;
+          for (int m = 0; m < NX; ++m) acc = fma(Acl[r * NX + m], dz[m], acc);
+          dxn[r] = acc;
         }
       };
       if constexpr (G <= 64) {
@@ -543,6 +546,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
           }
           xw.sync();
         }
+      }
+      // du_k = k_f + K dx_k on all lanes at once (the last node has no control)
+#pragma unroll
+      for (int l = 0; l < NU; ++l) {
+        double acc = kfk[l];
+#pragma unroll
+        for (int m = 0; m < NX; ++m) acc = fma(Kk[l * NX + m], dz[m], acc);
+        dz[NX + l] = (k < N) ? acc : 0.0;
       }
       // lambda+ = P_k dx_k + p_k (node-parallel, after the sequential sweep)
 #pragma unroll

@@ -44,7 +44,9 @@ def read_xlsx(path):
         row = []
         for c in r.findall(NS + "c"):
             v = c.find(NS + "v")
-            if v is None:
+            if c.get("t") == "inlineStr":
+                row.append("".join(t.text or "" for t in c.iter(NS + "t")))
+            elif v is None:
                 row.append(None)
             elif c.get("t") == "s":
                 row.append(shared[int(v.text)])

@@ -138,7 +138,9 @@ def test_casadi_call_shapes_and_closed_loop(mpcx, R, golden):
     state_target = np.array([10.0, 10.0, 0.0])
     w0 = [0.0] * (3 + 5 * N)
     mpc_iter = 0
+    t0 = 0.0
     states, controls = [], []
+    log = mpcx.ClosedLoopLog.for_ocp(ocp, state_init)  # cat_states / cat_controls / t (:210-270)
     while np.linalg.norm(state_init - state_target) > 1e-1 and mpc_iter * T < 20:
         args["p"] = np.concatenate([state_init, state_target])
         sol = solver(x0=w0, lbx=args["lbx"], ubx=args["ubx"], lbg=args["lbg"], ubg=args["ubg"], p=args["p"])
@@ -148,6 +150,8 @@ def test_casadi_call_shapes_and_closed_loop(mpcx, R, golden):
         X0 = np.array([sol["x"][0:3, 0]] + [sol["x"][5 + 5 * k:8 + 5 * k, 0] for k in range(N)]).T
         states.append(state_init.copy())
         controls.append(u[:, 0].copy())
+        log.record(sol["x"], t0)
+        t0 += T
         state_init = F(args["p"], u[:, 0])[0].reshape(-1)
         u0 = np.hstack([u[:, 1:], u[:, -1:]])
         X0 = np.hstack([X0[:, 1:], X0[:, -1:]])
@@ -161,6 +165,13 @@ def test_casadi_call_shapes_and_closed_loop(mpcx, R, golden):
     # the loop stops exactly where the reference's did: the state fed to the last solve
     # (row 84) is still > 0.1 away from the target, the state after it is not
     assert np.linalg.norm(states[-1] - state_target) > 1e-1 >= np.linalg.norm(state_init - state_target)
+    # the exported table (:316-334) equals 1exemplo.xlsx row for row
+    tab = log.table()
+    got = np.stack([tab[c] for c in ("x", "y", "theta", "v", "w", "t")], axis=1)
+    assert log.cat_states.shape == (3, N + 1, 85)
+    assert np.max(np.abs(got[:, 0:3] - rows[:, 0:3])) < 1e-6
+    assert rel_err(got[:, 3:5], rows[:, 3:5]) <= REL_TOL
+    np.testing.assert_allclose(got[:, 5], rows[:, 5], atol=1e-12)
 
 
 # ----------------------------------------------------------------------------- oracle parity at scale
