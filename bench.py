@@ -142,6 +142,17 @@ def cpu_baseline(make_P, N, steps, cores, min_seconds=10.0, max_reps=64, warm=(1
     return n / t_solve, t_solve, reps
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def _cold(P, N, nlp_ref):
     X = np.repeat(P[:, None, 0:3], N + 1, axis=1)
     return nlp_ref.join_w(X, np.zeros((P.shape[0], N, 2)))
@@ -313,12 +324,20 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu and cfg == 2:
         cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
         cores = max(1, min(cores, os.cpu_count() or 1))
-        rate, t, reps = cpu_baseline(lambda r: mdist.config2_inputs(r * B, (r + 1) * B, args.seed), N,
-                                     args.warmup + args.steps, cores, min_seconds=args.cpu_seconds)
+        make_P = lambda r: mdist.config2_inputs(r * B, (r + 1) * B, args.seed)  # noqa: E731
+        rate, t, reps = cpu_baseline(make_P, N, args.warmup + args.steps, cores, min_seconds=args.cpu_seconds)
+        # the reference's own loop is one solve at a time on one core (multiple_shooting_casadi.py:226-298)
+        B1 = 128
+        rate1, t1, reps1 = cpu_baseline(lambda r: make_P(r)[:B1], N, args.warmup + args.steps, 1,
+                                        min_seconds=args.cpu_seconds / 2)
         cpu = {"value": round(rate, 1), "unit": "solves/s", "cores": cores, "kind": "port",
                "sample": f"{reps} x ({args.warmup + args.steps}-step closed loop of {B} config-2 instances, "
                          f"N={N}, same warm start as the GPU loop); {t:.1f} s of timed solve calls on {cores} "
-                         "OpenMP threads"}
+                         "OpenMP threads",
+               "value_1core": round(rate1, 1),
+               "sample_1core": f"{reps1} x ({args.warmup + args.steps}-step closed loop of {B1} instances), "
+                               f"{t1:.1f} s on 1 thread",
+               "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
 
     if rank == 0:
         total = world * B * K

@@ -461,3 +461,35 @@ def test_integration_stub_runs():
     assert out.returncode == 0, out.stderr
     u = [float(v) for v in out.stdout.strip().strip("[]").split()]
     assert abs(u[0] - 1.0) < 1e-6 and abs(u[1] - math.pi / 4) < 1e-6
+
+
+# ----------------------------------------------------------------------------- committed golden vectors
+def test_rk4_sens_vs_committed_fixture(mpcx):
+    """Sweep kernel vs tests/golden/rk4_sens_random.npz (oracle outputs), <= 1e-12."""
+    import os
+
+    from conftest import ROOT
+
+    fx = np.load(os.path.join(ROOT, "tests", "golden", "rk4_sens_random.npz"))
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=20))
+    out = solver.rk4_sens(fx["w"], fx["P"])
+    for k in ("c", "q", "A", "B", "gq"):
+        scale = max(1.0, float(np.max(np.abs(fx[k]))))
+        assert np.max(np.abs(out[k] - fx[k])) <= 1e-12 * scale, k
+
+
+def test_n20_vs_committed_oracle_optima(mpcx):
+    """Config-2-shaped instances (N=20) vs tests/golden/unicycle_N20_oracle.npz: the
+    independent oracle's optima from the same cold start, within 1e-4 relative."""
+    import os
+
+    from conftest import ROOT
+
+    fx = np.load(os.path.join(ROOT, "tests", "golden", "unicycle_N20_oracle.npz"))
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=20))
+    r = solver.solve_batch(fx["P"])
+    assert np.all(r["status"] == 0)
+    same = [abs(r["f"][b] - fx["J"][b]) <= 1e-6 * max(1.0, abs(fx["J"][b])) for b in range(len(fx["J"]))]
+    assert np.mean(same) >= 0.9  # non-convex: an instance may settle in another local optimum
+    for b in np.flatnonzero(same):
+        assert rel_err(r["w"][b], fx["w"][b]) <= REL_TOL, b

@@ -145,3 +145,27 @@ def test_tracking_variant_node_cost():
     k3 = f(x + h / 2 * k2)
     k4 = f(x + h * k3)
     assert np.max(np.abs(xf - (x + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)))) < 1e-15
+
+
+def test_oracle_fixtures_regenerate():
+    """tests/golden/*.npz (SURVEY.md §8(c) golden vectors) are what the pinned oracle computes."""
+    import os
+    import sys
+
+    from conftest import ROOT
+
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_oracle_fixtures as M
+
+    rk = np.load(os.path.join(ROOT, "tests", "golden", "rk4_sens_random.npz"))
+    new = M.rk4_sens_case()
+    for k in ("P", "w", "c", "q", "A", "B", "gq"):
+        np.testing.assert_allclose(new[k], rk[k], rtol=1e-13, atol=1e-13, err_msg=k)
+    fx = np.load(os.path.join(ROOT, "tests", "golden", "unicycle_N20_oracle.npz"))
+    np.testing.assert_array_equal(M.n20_inputs(), fx["P"])
+    assert fx["converged"].all()
+    idx = [0, 3, 11, 30]
+    W, J, ok = M.n20_solve(fx["P"][idx])
+    assert ok.all()
+    np.testing.assert_allclose(W, fx["w"][idx], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(J, fx["J"][idx], rtol=1e-12)
