@@ -493,3 +493,19 @@ def test_n20_vs_committed_oracle_optima(mpcx):
     assert np.mean(same) >= 0.9  # non-convex: an instance may settle in another local optimum
     for b in np.flatnonzero(same):
         assert rel_err(r["w"][b], fx["w"][b]) <= REL_TOL, b
+
+
+def test_rk4_sens_pair_kernel_matches_scalar(mpcx):
+    """Even B takes the 16-B (two instances per lane) sweep; odd B the 8-B one.  Same
+    formulas per instance; the compiler may contract a sum differently in the two kernels,
+    so they agree to 1e-14 relative (each is within 1e-12 of the oracle above)."""
+    import os
+
+    from conftest import ROOT
+
+    fx = np.load(os.path.join(ROOT, "tests", "golden", "rk4_sens_random.npz"))
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=20))
+    odd = solver.rk4_sens(fx["w"], fx["P"])            # B = 37 -> scalar kernel
+    even = solver.rk4_sens(fx["w"][:36], fx["P"][:36])  # B = 36 -> pair kernel
+    for k in ("c", "q", "A", "B", "gq"):
+        np.testing.assert_allclose(even[k], odd[k][:36], rtol=1e-14, atol=1e-14, err_msg=k)

@@ -1,0 +1,110 @@
+// hbm_probe.hip -- streaming ceilings of one MI355X for the sweep's access mix (tools/, not product).
+//   write-only, read-only and a 1:4.5 read:write stream (the rk4_sens ratio: 848 B read per
+//   3840 B written per instance), all with 16-B per-lane accesses, >= 2 GB per pass so the
+//   256 MiB Infinity Cache cannot hold it.  hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); exit(1); } } while (0)
+
+__global__ void wr(double2* __restrict__ o, long n, double v) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    o[i] = make_double2(v, v + i);
+}
+__global__ void rd(const double2* __restrict__ a, long n, double* out) {
+  double s = 0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const double2 x = a[i];
+    s += x.x + x.y;
+  }
+  if (s == 1234.5) out[0] = s;
+}
+__global__ void wr_nt(double2* __restrict__ o, long n, double v) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    __builtin_nontemporal_store(v, &o[i].x);
+    __builtin_nontemporal_store(v + i, &o[i].y);
+  }
+}
+__global__ void wr_flat(double2* __restrict__ o, long n, double v) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i < n) o[i] = make_double2(v, v + i);
+}
+__global__ void wr8(double* __restrict__ o, long n, double v) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) o[i] = v + i;
+}
+// the sweep's store pattern, write only: B instances (2 per lane), S stages, 24 fields.
+// SoA: field row f*S... address ((k*24 + f) * B + b) -- rows B*8 bytes apart.
+__global__ void sweep_soa(double* __restrict__ o, int B, int S) {
+  const long b0 = 2 * ((long)blockIdx.x * blockDim.x + threadIdx.x);
+  if (b0 >= B) return;
+  for (int k = 0; k < S; ++k)
+#pragma unroll
+    for (int f = 0; f < 24; ++f)
+      *reinterpret_cast<double2*>(o + ((long)k * 24 + f) * B + b0) = make_double2(k + f, b0);
+}
+// tiled: per stage, each wave's 128 instances x 24 fields are one contiguous 24 KB block.
+__global__ void sweep_tiled(double* __restrict__ o, int B, int S) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long b0 = 2 * t;
+  if (b0 >= B) return;
+  const long tile = b0 / 128, lane2 = b0 % 128;
+  for (int k = 0; k < S; ++k)
+#pragma unroll
+    for (int f = 0; f < 24; ++f)
+      *reinterpret_cast<double2*>(o + (((long)k * (B / 128) + tile) * 24 + f) * 128 + lane2) = make_double2(k + f, b0);
+}
+// per element of `a`: 1 read, ~4.5 writes (9 writes per 2 reads)
+__global__ void mix(const double2* __restrict__ a, double2* __restrict__ o, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const double2 x = a[i];
+    const int reps = (i & 1) ? 5 : 4;
+    for (int r = 0; r < reps; ++r) o[(long)r * n + i] = make_double2(x.x + r, x.y - r);
+  }
+}
+
+int main() {
+  const long nw = (2L << 30) / 16;  // 2 GiB of double2
+  double2 *a, *o;
+  double* out;
+  CK(hipMalloc(&a, nw * 16));
+  CK(hipMalloc(&o, 5 * (nw / 4) * 16 + 16));
+  CK(hipMalloc(&out, 8));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int grid = 256 * 8 * 4, block = 256;
+  float ms;
+  auto timeit = [&](auto launch, double bytes, const char* name) {
+    launch();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < 10; ++r) launch();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("{\"probe\": \"%s\", \"GBps\": %.1f, \"ms\": %.4f}\n", name, bytes / (ms / 10 * 1e-3) / 1e9, ms / 10);
+  };
+  timeit([&] { hipLaunchKernelGGL(wr, dim3(grid), dim3(block), 0, 0, a, nw, 1.0); }, nw * 16.0, "write 16B/lane");
+  timeit([&] { hipLaunchKernelGGL(wr_nt, dim3(grid), dim3(block), 0, 0, a, nw, 1.0); }, nw * 16.0, "write nt 16B/lane");
+  timeit([&] { hipLaunchKernelGGL(wr_flat, dim3((unsigned)((nw + 255) / 256)), dim3(block), 0, 0, a, nw, 1.0); },
+         nw * 16.0, "write 16B/lane one element per thread");
+  timeit([&] { hipLaunchKernelGGL(wr8, dim3(grid), dim3(block), 0, 0, (double*)a, 2 * nw, 1.0); }, nw * 16.0,
+         "write 8B/lane");
+  timeit([&] { hipLaunchKernelGGL(rd, dim3(grid), dim3(block), 0, 0, a, nw, out); }, nw * 16.0, "read 16B/lane");
+  {
+    const int Bs = 1 << 19, S = 20;
+    double* ob;
+    CK(hipMalloc(&ob, (long)Bs * S * 24 * 8));
+    const double by = (double)Bs * S * 24 * 8;
+    timeit([&] { hipLaunchKernelGGL(sweep_soa, dim3(Bs / 2 / 256), dim3(256), 0, 0, ob, Bs, S); }, by,
+           "sweep store pattern SoA (rows 4 MB apart)");
+    timeit([&] { hipLaunchKernelGGL(sweep_tiled, dim3(Bs / 2 / 256), dim3(256), 0, 0, ob, Bs, S); }, by,
+           "sweep store pattern tiled (24 KB per wave per stage)");
+    CK(hipFree(ob));
+  }
+  const long nm = nw / 4;
+  timeit([&] { hipLaunchKernelGGL(mix, dim3(grid), dim3(block), 0, 0, a, o, nm); }, nm * 16.0 * (1 + 4.5),
+         "read:write 1:4.5 16B/lane");
+  return 0;
+}
