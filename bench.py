@@ -339,6 +339,17 @@ def main():
                                f"{t1:.1f} s on 1 thread",
                "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
 
+    # the kernel that dominates the timed step: the fused solve (+ plant/shift) launch.  Its HBM
+    # traffic is its inputs and outputs only, so neither HBM nor the FP64 pipes bound it: it is
+    # latency-bound on the sequential Riccati/forward chains (one wave per SIMD).
+    nw, ng, npar = solver._h.n_w, solver._h.n_g, solver._h.n_p
+    io_bytes = B * 8 * ((npar + 2 * nw + ng) + (nw + 1 + ng + nw) + (ocp.nx + 2 * nw + ng)) + B * 8
+    solve_info = {"kernel": "solve_kernel (fused IPM solve + plant/shift, one launch per step)",
+                  "bound": "latency: sequential Riccati/forward chains, one wave per SIMD",
+                  "ms_p50": round(p50, 4), "iters_max_per_step_mean": round(float(iters_max_step), 2),
+                  "us_per_ipm_iteration": round(p50 * 1e3 / max(iters_max_step, 1.0), 2),
+                  "hbm_bytes_per_launch": io_bytes,
+                  "hbm_frac": round(io_bytes / (p50 * 1e-3) / 1e9 / PEAK_HBM_GBS, 5)}
     if rank == 0:
         total = world * B * K
         out = {
@@ -353,7 +364,7 @@ def main():
             "iters_mean": round(float(S_all[:, 1].mean()), 2), "iters_max": int(S_all[:, 2].max()),
             "iters_max_per_step_mean": round(float(iters_max_step), 2),
             "failed_instances": int((S_all[:, 3] > 1).sum()),
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "solve_kernel": solve_info,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

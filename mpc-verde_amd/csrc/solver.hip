@@ -31,6 +31,9 @@
 // accounting of the solve loop (cdna_hip_programming.md §7 "In-kernel stamps").
 #ifdef MPCX_STAMPS
 __device__ unsigned long long* g_mpcx_stamps = nullptr;
+// per-instance event counters (diagnostic build; indices at the kernel's `diag` array)
+__device__ int* g_mpcx_diag = nullptr;
+#define DIAG(i) (++diag[(i)])
 #define STAMP(p)                                                                \
   do {                                                                          \
     __builtin_amdgcn_sched_barrier(0);                                          \
@@ -44,6 +47,9 @@ __device__ unsigned long long* g_mpcx_stamps = nullptr;
 #else
 #define STAMP(p) \
   do {           \
+  } while (0)
+#define DIAG(i) \
+  do {          \
   } while (0)
 #endif
 
@@ -88,8 +94,13 @@ __device__ __forceinline__ double barrier_logsum(const double* z, const double* 
   return log(m) + (double)e * 0.69314718055994530942;
 }
 
+#ifndef MPCX_WAVES_PER_EU
+#define MPCX_WAVES_ATTR
+#else
+#define MPCX_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(MPCX_WAVES_PER_EU, MPCX_WAVES_PER_EU)))
+#endif
 template <class Model, int G>
-__global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
+__global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(SolveArgs a) {
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2, NP = NX * (NX + 1) / 2;
   static_assert(NP + NX <= kXchStride && 2 * NZ + NX <= kXchStride, "LDS exchange slot too small");
   const int lane = threadIdx.x & 63;
@@ -239,6 +250,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
   double Pk[NP] = {}, pk[NX] = {}, Kk[NU * NX] = {}, kfk[NU] = {};
 
 #ifdef MPCX_STAMPS
+  // 0 regularised iterations, 1 extra factorisations, 2 backtracks, 3 barrier updates,
+  // 4 fraction-to-boundary-limited steps (alpha_max < 1), 5 tiny steps, 6 filter rejections,
+  // 7 f-type (Armijo) acceptances
+  int diag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = 0;
   int st_ph = 9;
@@ -358,6 +373,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
       Ecm = gmax<G>(Ecm, xw);
       const double Emu = fmax(fmax(Ed / sd, Ec), Ecm / sc);
       const bool dec = !done && Emu <= kKappaEps * mu && mu > mu_min;
+      if (dec && !done) DIAG(3);
       if (dec) {
         static_assert(kThetaMu == 1.5, "mu^theta_mu evaluated as mu * sqrt(mu)");
         mu = fmax(mu_min, fmin(kKappaMu * mu, mu * sqrt(mu)));
@@ -464,7 +480,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
         if (ok) {
           need = false;
           if (delta > 0.0) dw_last = delta;
+          if (delta > 0.0) DIAG(0);
         } else {
+          DIAG(1);
           if (first) delta = dw_last == 0.0 ? kDw0 : fmax(kDwMin, kKwMinus * dw_last);
           else delta *= dw_last == 0.0 ? kKwPlusBar : kKwPlus;
           first = false;
@@ -596,6 +614,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
       }
     }
     const double amax = gmin<G>(amax_l, xw), az = gmin<G>(az_l, xw), tiny = gmax<G>(tiny_l, xw);
+    if (!done && amax < 1.0) DIAG(4);
+    if (!done && tiny < 10.0 * kEps) DIAG(5);
     const double gd = gsum<G>(gd_l, xw);
 
     STAMP(6);
@@ -649,11 +669,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
             acc = tht <= (1.0 - kGammaTheta) * thk || pht <= phk - kGammaPhi * thk + 10.0 * kEps * fabs(phk);
           }
         }
+        if (searching && infilter) DIAG(6);
         if (acc) {
           searching = false;
           accepted = true;
           ftype = ft;
+          if (ft) DIAG(7);
         } else {
+          DIAG(2);
           alpha *= 0.5;
           if (alpha < amin) searching = false;  // would need restoration
         }
@@ -695,6 +718,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) void solve_kernel(SolveArgs a) {
   }
   STAMP(9);
 #ifdef MPCX_STAMPS
+  if (g_mpcx_diag && valid && k == 0)
+    for (int i = 0; i < 8; ++i) g_mpcx_diag[(size_t)inst * 8 + i] = diag[i];
   if (g_mpcx_stamps && (threadIdx.x & 63) == 0) {
     const long wv = gid / 64;
     for (int i = 0; i < 10; ++i) g_mpcx_stamps[wv * 10 + i] = st_acc[i];
@@ -977,6 +1002,9 @@ __global__ void constraints_kernel(SolveArgs a, const double* __restrict__ W, do
 #ifdef MPCX_STAMPS
 extern "C" int mpcx_diag_set_stamp_buffer(void* d_buf) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_mpcx_stamps), &d_buf, sizeof(void*));
+}
+extern "C" int mpcx_diag_set_counter_buffer(void* d_buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_mpcx_diag), &d_buf, sizeof(void*));
 }
 #endif
 
