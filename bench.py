@@ -159,26 +159,26 @@ def _cold(P, N, nlp_ref):
 
 
 def sweep_roofline(solver, torch, B, N, reps, stream):
-    """Time the rk4_sens sweep kernel at B instances (SoA buffers resident in HBM)."""
+    """Time the rk4_sens sweep kernel at B instances (tiled SoA buffers resident in HBM)."""
     from mpcx import _lib
     import ctypes
 
     dev = torch.device("cuda", torch.cuda.current_device())
     g = torch.Generator(device="cpu").manual_seed(7)
-    X = torch.empty(((N + 1) * 3, B), dtype=torch.float64)
-    X[0::3].uniform_(-10, 10, generator=g)
-    X[1::3].uniform_(-10, 10, generator=g)
-    X[2::3].uniform_(-3.14, 3.14, generator=g)
-    U = torch.empty((N * 2, B), dtype=torch.float64).uniform_(-0.78, 0.78, generator=g)
-    XR = torch.empty((3, B), dtype=torch.float64).uniform_(-10, 10, generator=g)
+    T = (B + 63) // 64  # tiled SoA (include/mpcx.h: mpcx_rk4_sens_dev): [stage][tile][field][64]
+    X = torch.empty((N + 1, T, 3, 64), dtype=torch.float64)
+    X[:, :, 0:2].uniform_(-10, 10, generator=g)
+    X[:, :, 2].uniform_(-3.14, 3.14, generator=g)
+    U = torch.empty((N, T, 2, 64), dtype=torch.float64).uniform_(-0.78, 0.78, generator=g)
+    XR = torch.empty((1, T, 3, 64), dtype=torch.float64).uniform_(-10, 10, generator=g)
     X, U, XR = X.to(dev), U.to(dev), XR.to(dev)
-    outs = [torch.empty((N * m, B), dtype=torch.float64, device=dev) for m in (3, 1, 9, 6, 5)]
+    J = torch.empty((N, T, 24, 64), dtype=torch.float64, device=dev)  # per-interval records
     lib = _lib.load()
     vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     s = ctypes.c_void_p(stream.cuda_stream)
 
     def launch():
-        _lib.check(lib.mpcx_rk4_sens_dev(solver._h.ptr, B, vp(X), vp(U), vp(XR), *[vp(o) for o in outs], s))
+        _lib.check(lib.mpcx_rk4_sens_dev(solver._h.ptr, B, vp(X), vp(U), vp(XR), vp(J), s))
 
     for _ in range(3):
         launch()
@@ -191,7 +191,7 @@ def sweep_roofline(solver, torch, B, N, reps, stream):
     e1.record(stream)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    del X, U, XR, outs
+    del X, U, XR, J
     torch.cuda.empty_cache()
     return ms
 

@@ -200,13 +200,15 @@ int mpcx_step_dev(mpcx_handle* h, int32_t B, double* d_P, double* d_w0, double* 
 int mpcx_rk4_sens(mpcx_handle* h, int32_t B, const double* w, const double* P, double* c, double* q, double* A,
                   double* Bm, double* gq);
 
-/* Device variant of the sweep on structure-of-arrays buffers (the layout the
-   kernel streams from HBM):
- *   d_X  (N+1) x nx x B,  d_U  N x nu x B,  d_xr nx x B      (inputs)
- *   d_c  N x nx x B, d_q N x B, d_A N x nx*nx x B, d_Bm N x nx*nu x B,
- *   d_gq N x (nx+nu) x B                                      (outputs)       */
+/* Device variant of the sweep on tiled structure-of-arrays buffers (the layout the
+   kernel streams from HBM).  Instances are grouped in T = ceil(B/64)
+   tiles of 64; an array with S stages and F fields per stage holds element
+   (stage s, field i, instance b) at  ((s*T + b/64)*F + i)*64 + b%64  (size S*T*F*64):
+ *   d_X  S=N+1, F=nx;  d_U  S=N, F=nu;  d_xr  S=1, F=nx          (inputs)
+ *   d_J  S=N, F=24: the per-interval record, fields
+ *        0-2 c (defect), 3 q, 4-12 A (row-major), 13-18 Bm (row-major), 19-23 gq  (output) */
 int mpcx_rk4_sens_dev(mpcx_handle* h, int32_t B, const double* d_X, const double* d_U, const double* d_xr,
-                      double* d_c, double* d_q, double* d_A, double* d_Bm, double* d_gq, void* stream);
+                      double* d_J, void* stream);
 
 #ifdef __cplusplus
 }

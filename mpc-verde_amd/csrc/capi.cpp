@@ -478,14 +478,13 @@ int mpcx_shift_dev(mpcx_handle* h, int32_t B, double* d_P, const double* d_w, do
 }
 
 int mpcx_rk4_sens_dev(mpcx_handle* h, int32_t B, const double* d_X, const double* d_U, const double* d_xr,
-                      double* d_c, double* d_q, double* d_A, double* d_Bm, double* d_gq, void* stream) {
-  if (!h || !d_X || !d_U || !d_xr || !d_c || !d_q || !d_A || !d_Bm || !d_gq) return fail(MPCX_EINVAL, "null argument");
+                      double* d_J, void* stream) {
+  if (!h || !d_X || !d_U || !d_xr || !d_J) return fail(MPCX_EINVAL, "null argument");
   if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
   if (h->spec.model != MPCX_MODEL_UNICYCLE || h->spec.param_layout != MPCX_P_X0_XREF)
     return fail(MPCX_EINVAL, "rk4_sens_dev: unicycle model with param_layout X0_XREF only");
   HIPCHK(hipSetDevice(h->spec.device));
-  HIPCHK(mpcx::launch_rk4_sens(B, h->spec.N, stage_params(h->spec), d_X, d_U, d_xr, d_c, d_q, d_A, d_Bm, d_gq,
-                               (hipStream_t)stream));
+  HIPCHK(mpcx::launch_rk4_sens(B, h->spec.N, stage_params(h->spec), d_X, d_U, d_xr, d_J, (hipStream_t)stream));
   return 0;
 }
 
@@ -497,10 +496,13 @@ int mpcx_rk4_sens(mpcx_handle* h, int32_t B, const double* w, const double* P, d
     return fail(MPCX_EINVAL, "rk4_sens: unicycle model with param_layout X0_XREF only");
   HIPCHK(hipSetDevice(h->spec.device));
   const int N = h->spec.N;
-  const size_t nX = (size_t)(N + 1) * 3 * B, nU = (size_t)N * 2 * B, nR = (size_t)3 * B;
-  const size_t nC = (size_t)N * 3 * B, nQ = (size_t)N * B, nA = (size_t)N * 9 * B, nB = (size_t)N * 6 * B,
-               nG = (size_t)N * 5 * B;
-  const size_t total = nX + nU + nR + nC + nQ + nA + nB + nG;
+  const long T = ((long)B + 63) / 64, Bp = T * 64;  // 64-instance tiles (mpcx_rk4_sens_dev layout)
+  auto tix = [T](int stage, int F, int i, long b) {
+    return (((size_t)stage * T + (b >> 6)) * F + i) * 64 + (b & 63);
+  };
+  const size_t nX = (size_t)(N + 1) * 3 * Bp, nU = (size_t)N * 2 * Bp, nR = (size_t)3 * Bp;
+  const size_t nJ = (size_t)N * 24 * Bp;
+  const size_t total = nX + nU + nR + nJ;
   if (total > h->cap_sweep) {
     (void)hipFree(h->d_sweep);
     h->d_sweep = nullptr;
@@ -508,38 +510,33 @@ int mpcx_rk4_sens(mpcx_handle* h, int32_t B, const double* w, const double* P, d
     HIPCHK(hipMalloc(&h->d_sweep, total * sizeof(double)));
     h->cap_sweep = total;
   }
-  std::vector<double> hX(nX), hU(nU), hR(nR);
+  std::vector<double> hX(nX, 0.0), hU(nU, 0.0), hR(nR, 0.0);
   for (int b = 0; b < B; ++b) {
     const double* wb = w + (size_t)b * h->nw;
     for (int k = 0; k <= N; ++k)
-      for (int i = 0; i < 3; ++i) hX[((size_t)k * 3 + i) * B + b] = k == 0 ? wb[i] : wb[3 + 5 * (k - 1) + 2 + i];
+      for (int i = 0; i < 3; ++i) hX[tix(k, 3, i, b)] = k == 0 ? wb[i] : wb[3 + 5 * (k - 1) + 2 + i];
     for (int k = 0; k < N; ++k)
-      for (int i = 0; i < 2; ++i) hU[((size_t)k * 2 + i) * B + b] = wb[3 + 5 * k + i];
-    for (int i = 0; i < 3; ++i) hR[(size_t)i * B + b] = P[(size_t)b * h->np + 3 + i];
+      for (int i = 0; i < 2; ++i) hU[tix(k, 2, i, b)] = wb[3 + 5 * k + i];
+    for (int i = 0; i < 3; ++i) hR[tix(0, 3, i, b)] = P[(size_t)b * h->np + 3 + i];
   }
   double* d = h->d_sweep;
-  double *dX = d, *dU = dX + nX, *dR = dU + nU, *dC = dR + nR, *dQ = dC + nC, *dA = dQ + nQ, *dB = dA + nA,
-         *dG = dB + nB;
+  double *dX = d, *dU = dX + nX, *dR = dU + nU, *dJ = dR + nR;
   hipStream_t s = h->stream;
   HIPCHK(hipMemcpyAsync(dX, hX.data(), nX * sizeof(double), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(dU, hU.data(), nU * sizeof(double), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(dR, hR.data(), nR * sizeof(double), hipMemcpyHostToDevice, s));
-  HIPCHK(mpcx::launch_rk4_sens(B, N, stage_params(h->spec), dX, dU, dR, dC, dQ, dA, dB, dG, s));
-  std::vector<double> hC(nC), hQ(nQ), hA(nA), hB(nB), hG(nG);
-  HIPCHK(hipMemcpyAsync(hC.data(), dC, nC * sizeof(double), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(hQ.data(), dQ, nQ * sizeof(double), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(hA.data(), dA, nA * sizeof(double), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(hB.data(), dB, nB * sizeof(double), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(hG.data(), dG, nG * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(mpcx::launch_rk4_sens(B, N, stage_params(h->spec), dX, dU, dR, dJ, s));
+  std::vector<double> hJ(nJ);
+  HIPCHK(hipMemcpyAsync(hJ.data(), dJ, nJ * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   for (int b = 0; b < B; ++b)
     for (int k = 0; k < N; ++k) {
       const size_t o = (size_t)b * N + k;
-      for (int i = 0; i < 3; ++i) c[o * 3 + i] = hC[((size_t)k * 3 + i) * B + b];
-      q[o] = hQ[(size_t)k * B + b];
-      for (int i = 0; i < 9; ++i) A[o * 9 + i] = hA[((size_t)k * 9 + i) * B + b];
-      for (int i = 0; i < 6; ++i) Bm[o * 6 + i] = hB[((size_t)k * 6 + i) * B + b];
-      for (int i = 0; i < 5; ++i) gq[o * 5 + i] = hG[((size_t)k * 5 + i) * B + b];
+      for (int i = 0; i < 3; ++i) c[o * 3 + i] = hJ[tix(k, 24, i, b)];
+      q[o] = hJ[tix(k, 24, 3, b)];
+      for (int i = 0; i < 9; ++i) A[o * 9 + i] = hJ[tix(k, 24, 4 + i, b)];
+      for (int i = 0; i < 6; ++i) Bm[o * 6 + i] = hJ[tix(k, 24, 13 + i, b)];
+      for (int i = 0; i < 5; ++i) gq[o * 5 + i] = hJ[tix(k, 24, 19 + i, b)];
     }
   return 0;
 }

@@ -58,7 +58,7 @@ __host__ __device__ inline ModelArgs model_args(const SolveArgs& a) { return Mod
 
 hipError_t launch_solve(const SolveArgs& a, hipStream_t stream);
 hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X, const double* U, const double* XR,
-                           double* C, double* Q, double* A, double* Bm, double* G, hipStream_t stream);
+                           double* J, hipStream_t stream);
 // plant: x+ = F(x0, u) for B instances (stage-0 model of each instance)
 hipError_t launch_plant(const SolveArgs& a, const double* U, double* XF, double* QF, hipStream_t stream);
 // closed-loop shift (plant + shifted warm start of primal and multipliers)

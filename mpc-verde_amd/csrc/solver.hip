@@ -801,120 +801,54 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 }
 
 // ------------------------------------------------------------------------------
-// RK4 + Jacobian sweep over B x N unicycle intervals, structure-of-arrays streams.
+// RK4 + Jacobian sweep over B x N unicycle intervals, tiled structure of arrays.
 // One thread per instance walks its N intervals: X_{k+1} loaded for interval k stays in
 // registers as interval k+1's X_k and x_ref is loaded once, so HBM sees exactly the
 // compulsory bytes (reads (N+1)*3 + 2N + 3 doubles, writes 24N doubles per instance;
-// DESIGN.md §4).  Consecutive lanes = consecutive instances: every load/store of a wave
-// is one contiguous 512-B segment.
+// DESIGN.md §4).  Layout: 64-instance tiles, tile index inside each stage (tix below), so
+// every wave's loads/stores of one stage are contiguous 512-B rows of one block -- the
+// store pattern HBM absorbs fastest on this part (tools/hbm_probe.hip).
 // ------------------------------------------------------------------------------
+constexpr int kRec = 24;  // fields of the per-stage sweep record
+__device__ __forceinline__ size_t tix(int stage, int F, int i, long b, long T) {
+  return (((size_t)stage * T + (b >> 6)) * F + i) * 64 + (b & 63);
+}
+
 __global__ __launch_bounds__(256) void rk4_sens_kernel(int B, int N, StageParams sp, const double* __restrict__ X,
                                                        const double* __restrict__ U, const double* __restrict__ XR,
-                                                       double* __restrict__ C, double* __restrict__ Qo,
-                                                       double* __restrict__ Ao, double* __restrict__ Bo,
-                                                       double* __restrict__ Go) {
+                                                       double* __restrict__ J) {
   const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  const long Bl = B;
+  const long T = ((long)B + 63) / 64;
   double x[3], xr[3];
   const double ur[2] = {0.0, 0.0};
   const double lz[3] = {0, 0, 0};
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    x[i] = X[i * Bl + b];
-    xr[i] = XR[i * Bl + b];
+    x[i] = X[tix(0, 3, i, b, T)];
+    xr[i] = XR[tix(0, 3, i, b, T)];
   }
   for (int k = 0; k < N; ++k) {
     double u[2], xn[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) xn[i] = X[((long)(k + 1) * 3 + i) * Bl + b];
+    for (int i = 0; i < 3; ++i) xn[i] = X[tix(k + 1, 3, i, b, T)];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) u[i] = U[((long)k * 2 + i) * Bl + b];
+    for (int i = 0; i < 2; ++i) u[i] = U[tix(k, 2, i, b, T)];
     double xf[3], q, A[9], Bm[6], g[5], H[15];
     uni_derivs<false>(sp, x, u, xr, ur, lz, 1.0, xf, q, A, Bm, g, H);
+    // one 24-field record per stage: c(3) q(1) A(9) B(6) grad q(5) -- a wave's whole
+    // output of a stage is one contiguous 12 KB block
 #pragma unroll
-    for (int i = 0; i < 3; ++i) C[((long)k * 3 + i) * Bl + b] = xf[i] - xn[i];
-    Qo[(long)k * Bl + b] = q;
+    for (int i = 0; i < 3; ++i) J[tix(k, kRec, i, b, T)] = xf[i] - xn[i];
+    J[tix(k, kRec, 3, b, T)] = q;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) Ao[((long)k * 9 + i) * Bl + b] = A[i];
+    for (int i = 0; i < 9; ++i) J[tix(k, kRec, 4 + i, b, T)] = A[i];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) Bo[((long)k * 6 + i) * Bl + b] = Bm[i];
+    for (int i = 0; i < 6; ++i) J[tix(k, kRec, 13 + i, b, T)] = Bm[i];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) Go[((long)k * 5 + i) * Bl + b] = g[i];
+    for (int i = 0; i < 5; ++i) J[tix(k, kRec, 19 + i, b, T)] = g[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i) x[i] = xn[i];
-  }
-}
-
-// The same sweep with 16-B accesses: each lane owns two adjacent instances (b0, b0+1), so
-// every load and store is a double2 (a wave moves 1 KB per instruction; 8-B/lane streams
-// run at 0.54-0.70x the 16-B rate on gfx950).  Layout and results are identical to
-// rk4_sens_kernel; requires even B and 16-B aligned buffers (checked by the launcher).
-__global__ __launch_bounds__(256) void rk4_sens_kernel2(int B, int N, StageParams sp, const double* __restrict__ X,
-                                                        const double* __restrict__ U, const double* __restrict__ XR,
-                                                        double* __restrict__ C, double* __restrict__ Qo,
-                                                        double* __restrict__ Ao, double* __restrict__ Bo,
-                                                        double* __restrict__ Go) {
-  const long b0 = 2 * ((long)blockIdx.x * blockDim.x + threadIdx.x);
-  if (b0 >= B) return;
-  const long Bl = B;
-  auto ld2 = [&](const double* base, long row) { return *reinterpret_cast<const double2*>(base + row * Bl + b0); };
-  auto st2 = [&](double* base, long row, double a, double b) {
-    *reinterpret_cast<double2*>(base + row * Bl + b0) = make_double2(a, b);
-  };
-  double x[2][3], xr[2][3];
-  const double ur[2] = {0.0, 0.0};
-  const double lz[3] = {0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const double2 v = ld2(X, i), r = ld2(XR, i);
-    x[0][i] = v.x;
-    x[1][i] = v.y;
-    xr[0][i] = r.x;
-    xr[1][i] = r.y;
-  }
-  for (int k = 0; k < N; ++k) {
-    double u[2][2], xn[2][3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const double2 v = ld2(X, (long)(k + 1) * 3 + i);
-      xn[0][i] = v.x;
-      xn[1][i] = v.y;
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const double2 v = ld2(U, (long)k * 2 + i);
-      u[0][i] = v.x;
-      u[1][i] = v.y;
-    }
-    double o[2][24];  // c(3) q(1) A(9) B(6) g(5) of both instances
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      double xf[3], q, A[9], Bm[6], g[5], H[15];
-      uni_derivs<false>(sp, x[j], u[j], xr[j], ur, lz, 1.0, xf, q, A, Bm, g, H);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) o[j][i] = xf[i] - xn[j][i];
-      o[j][3] = q;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) o[j][4 + i] = A[i];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) o[j][13 + i] = Bm[i];
-#pragma unroll
-      for (int i = 0; i < 5; ++i) o[j][19 + i] = g[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) st2(C, (long)k * 3 + i, o[0][i], o[1][i]);
-    st2(Qo, k, o[0][3], o[1][3]);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) st2(Ao, (long)k * 9 + i, o[0][4 + i], o[1][4 + i]);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) st2(Bo, (long)k * 6 + i, o[0][13 + i], o[1][13 + i]);
-#pragma unroll
-    for (int i = 0; i < 5; ++i) st2(Go, (long)k * 5 + i, o[0][19 + i], o[1][19 + i]);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 3; ++i) x[j][i] = xn[j][i];
   }
 }
 
@@ -1067,17 +1001,9 @@ hipError_t launch_shift(const SolveArgs& a, double* P, const double* W, double* 
 }
 
 hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X, const double* U, const double* XR,
-                           double* C, double* Q, double* A, double* Bm, double* G, hipStream_t stream) {
-  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if ((B & 1) == 0 && al16(X) && al16(U) && al16(XR) && al16(C) && al16(Q) && al16(A) && al16(Bm) && al16(G)) {
-    const long blocks = ((long)B / 2 + 255) / 256;
-    hipLaunchKernelGGL(rk4_sens_kernel2, dim3((unsigned)blocks), dim3(256), 0, stream, B, N, sp, X, U, XR, C, Q, A,
-                       Bm, G);
-  } else {
-    const long blocks = ((long)B + 255) / 256;
-    hipLaunchKernelGGL(rk4_sens_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, B, N, sp, X, U, XR, C, Q, A,
-                       Bm, G);
-  }
+                           double* J, hipStream_t stream) {
+  const long blocks = ((long)B + 255) / 256;
+  hipLaunchKernelGGL(rk4_sens_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, B, N, sp, X, U, XR, J);
   return hipGetLastError();
 }
 

@@ -98,7 +98,7 @@ def load():
     lib.mpcx_plant_step.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp]
     lib.mpcx_shift_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mpcx_rk4_sens.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp, dp, dp, dp]
-    lib.mpcx_rk4_sens_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.mpcx_rk4_sens_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp]
     lib.mpcx_set_linear_model.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp, ip, ctypes.c_int32]
     lib.mpcx_set_linear_tab_dev.argtypes = [H, ctypes.c_void_p, ctypes.c_int32]
     lib.mpcx_step_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp]

@@ -495,17 +495,19 @@ def test_n20_vs_committed_oracle_optima(mpcx):
         assert rel_err(r["w"][b], fx["w"][b]) <= REL_TOL, b
 
 
-def test_rk4_sens_pair_kernel_matches_scalar(mpcx):
-    """Even B takes the 16-B (two instances per lane) sweep; odd B the 8-B one.  Same
-    formulas per instance; the compiler may contract a sum differently in the two kernels,
-    so they agree to 1e-14 relative (each is within 1e-12 of the oracle above)."""
+def test_rk4_sens_ragged_tiles(mpcx):
+    """B not a multiple of the 64-instance tile (partial last tile) and B > 64: every
+    instance's outputs equal those of the same instance solved alone (bit-identical)."""
     import os
 
     from conftest import ROOT
 
     fx = np.load(os.path.join(ROOT, "tests", "golden", "rk4_sens_random.npz"))
     solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=20))
-    odd = solver.rk4_sens(fx["w"], fx["P"])            # B = 37 -> scalar kernel
-    even = solver.rk4_sens(fx["w"][:36], fx["P"][:36])  # B = 36 -> pair kernel
+    w = np.concatenate([fx["w"]] * 3)  # B = 111: tiles of 64 + 47
+    P = np.concatenate([fx["P"]] * 3)
+    big = solver.rk4_sens(w, P)
+    one = solver.rk4_sens(fx["w"][5:6], fx["P"][5:6])
     for k in ("c", "q", "A", "B", "gq"):
-        np.testing.assert_allclose(even[k], odd[k][:36], rtol=1e-14, atol=1e-14, err_msg=k)
+        for b in (5, 42, 79):
+            np.testing.assert_array_equal(big[k][b], one[k][0], err_msg=k)

@@ -54,6 +54,26 @@ __global__ void sweep_tiled(double* __restrict__ o, int B, int S) {
     for (int f = 0; f < 24; ++f)
       *reinterpret_cast<double2*>(o + (((long)k * (B / 128) + tile) * 24 + f) * 128 + lane2) = make_double2(k + f, b0);
 }
+// tile-major: each wave's whole output (S stages x 24 fields x 128) is one contiguous region
+__global__ void sweep_tilemajor(double* __restrict__ o, int B, int S) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long b0 = 2 * t;
+  if (b0 >= B) return;
+  const long tile = b0 / 128, lane2 = b0 % 128;
+  for (int k = 0; k < S; ++k)
+#pragma unroll
+    for (int f = 0; f < 24; ++f)
+      *reinterpret_cast<double2*>(o + ((tile * S + k) * 24 + f) * 128 + lane2) = make_double2(k + f, b0);
+}
+// tiled with 64-instance tiles (8-B per lane, one instance per lane)
+__global__ void sweep_tiled64(double* __restrict__ o, int B, int S) {
+  const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const long tile = b / 64, lane = b % 64;
+  for (int k = 0; k < S; ++k)
+#pragma unroll
+    for (int f = 0; f < 24; ++f) o[(((long)k * (B / 64) + tile) * 24 + f) * 64 + lane] = k + f + b;
+}
 // per element of `a`: 1 read, ~4.5 writes (9 writes per 2 reads)
 __global__ void mix(const double2* __restrict__ a, double2* __restrict__ o, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -101,6 +121,10 @@ int main() {
            "sweep store pattern SoA (rows 4 MB apart)");
     timeit([&] { hipLaunchKernelGGL(sweep_tiled, dim3(Bs / 2 / 256), dim3(256), 0, 0, ob, Bs, S); }, by,
            "sweep store pattern tiled (24 KB per wave per stage)");
+    timeit([&] { hipLaunchKernelGGL(sweep_tilemajor, dim3(Bs / 2 / 256), dim3(256), 0, 0, ob, Bs, S); }, by,
+           "sweep store pattern tile-major (480 KB per wave)");
+    timeit([&] { hipLaunchKernelGGL(sweep_tiled64, dim3(Bs / 256), dim3(256), 0, 0, ob, Bs, S); }, by,
+           "sweep store pattern tiled, 64-instance tiles, 8B/lane");
     CK(hipFree(ob));
   }
   const long nm = nw / 4;
