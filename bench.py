@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU (default per config)")
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--mode", choices=("async", "lockstep"), default="async",
+                    help="async: the K timed steps run as ONE multi-step launch (instances independent); "
+                         "lockstep: one launch per step")
     ap.add_argument("--roofline-batch", type=int, default=1 << 19)
     ap.add_argument("--roofline-reps", type=int, default=20)
     ap.add_argument("--no-roofline", action="store_true")
@@ -140,6 +143,16 @@ def cpu_baseline(make_P, N, steps, cores, min_seconds=10.0, max_reps=64, warm=(1
             lamx0 = shift_lamx_np(r["lam_x"], N)
         reps += 1
     return n / t_solve, t_solve, reps
+
+
+def _pseq(refs, n_p, nx):
+    """(K, B, n_p) full parameter rows from (K, B, n_p - nx) stage references (x0 unused)."""
+    import torch
+
+    K, B = refs.shape[0], refs.shape[1]
+    out = torch.zeros((K, B, n_p), dtype=torch.float64, device=refs.device)
+    out[:, :, nx:] = refs
+    return out
 
 
 def cpu_model():
@@ -228,8 +241,9 @@ def main():
     N = args.N or {2: 20, 3: 30, 4: 50, 5: 100}[cfg]
     B = args.batch or {2: 1024, 3: 4096, 4: 1024, 5: 2048}[cfg]
     start, stop = mdist.shard(B, rank)
-    T_all = args.warmup + args.steps
+    T_all = args.warmup + 2 * args.steps  # warmup, timed multi-step run, lock-step latency run
     per_step = None  # per-step device updates (stage references / schedules), resident in HBM
+    seq = lambda t0, K: (None, None)  # noqa: E731  same, as sequences for a multi-step launch
     if cfg in (2, 3):
         ocp = mpcx.unicycle_point_to_point(N=N) if cfg == 2 else mpcx.unicycle_tracking(N=N)
     elif cfg == 4:
@@ -254,6 +268,7 @@ def main():
         refs = torch.from_numpy(np.stack([mpcx.ocp.circular_reference(tau0, t, N).reshape(B, -1)
                                           for t in range(T_all)])).to(dev)
         per_step = lambda lp, t: lp.set_stage_refs(refs[t])  # noqa: E731
+        seq = lambda t0, K: (_pseq(refs[t0:t0 + K], P0.shape[1], 3), None)  # noqa: E731
     elif cfg == 4:  # instance time t0 + t: references par[t] and the model re-linearised at vref[t] (:117-141)
         tt = np.minimum(t0[None, :] + np.arange(T_all)[:, None], 499)  # (T_all, B)
         refs = torch.from_numpy(np.ascontiguousarray(par[tt].reshape(T_all, B, -1))).to(dev)
@@ -263,6 +278,8 @@ def main():
         def per_step(lp, t):
             lp.set_stage_refs(refs[t])
             lp.set_schedule(tabs[t])
+
+        seq = lambda t0, K: (_pseq(refs[t0:t0 + K], P0.shape[1], 4), tabs[t0:t0 + K].contiguous())  # noqa: E731
     else:
         P0 = mpcx.lti.pendulum_params(ocp, mdist.config5_inputs(start, stop), 0.0)
     loop = DeviceLoop(solver, P0, device=dev, stream=stream)
@@ -273,26 +290,50 @@ def main():
         loop.step()
     torch.cuda.synchronize()
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     iters_hist = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
     status_hist = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
+    t_seq = args.warmup
+    if per_step is not None:
+        per_step(loop, t_seq)  # current references / schedule = those of the first timed step
+    Pseq, tabseq = seq(t_seq, K)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(K):
-        if per_step is not None:
-            per_step(loop, args.warmup + i)
-        ev[i][0].record(stream)
-        loop.step(status_out=status_hist[i], iters_out=iters_hist[i])  # solve + plant/shift, one launch
-        ev[i][1].record(stream)
+    if args.mode == "async":
+        # K closed-loop steps in ONE launch; every instance runs its own receding-horizon loop
+        # (bit-identical to K lock-step launches, tests/test_gpu_parity.py::test_run_*)
+        loop.run(K, status_out=status_hist, iters_out=iters_hist, Pseq=Pseq, tabseq=tabseq)
+    else:
+        for i in range(K):
+            if per_step is not None and i > 0:
+                per_step(loop, t_seq + i)
+            loop.step(status_out=status_hist[i], iters_out=iters_hist[i])
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         torch.distributed.barrier()
     elapsed = mdist.max_over_ranks(t1 - t0, device=loop.P.device)
+
+    # lock-step latency: K further steps, one launch each, HIP events on the launch stream
+    # (ms_per_solve_p50 = the latency a real-time loop sees per closed-loop step)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    lk_st = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
+    lk_it = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
+    torch.cuda.synchronize()
+    tl0 = time.perf_counter()
+    for i in range(K):
+        if per_step is not None:
+            per_step(loop, args.warmup + K + i)
+        ev[i][0].record(stream)
+        loop.step(status_out=lk_st[i], iters_out=lk_it[i])
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    tl1 = time.perf_counter()
+    lock_elapsed = mdist.max_over_ranks(tl1 - tl0, device=loop.P.device)
     solve_ms = sorted(a.elapsed_time(b) for a, b in ev)
     p50 = mdist.max_over_ranks(float(np.median(solve_ms)), device=loop.P.device)
+    lock_iters_max = mdist.max_over_ranks(float(lk_it.max(dim=1).values.double().mean().item()), device=loop.P.device)
 
     # closed-loop statistics: the only collective (RCCL all_gather over xGMI), outside the timed region
     P_fin = loop.P.cpu().numpy()
@@ -346,8 +387,8 @@ def main():
     io_bytes = B * 8 * ((npar + 2 * nw + ng) + (nw + 1 + ng + nw) + (ocp.nx + 2 * nw + ng)) + B * 8
     solve_info = {"kernel": "solve_kernel (fused IPM solve + plant/shift, one launch per step)",
                   "bound": "latency: sequential Riccati/forward chains, one wave per SIMD",
-                  "ms_p50": round(p50, 4), "iters_max_per_step_mean": round(float(iters_max_step), 2),
-                  "us_per_ipm_iteration": round(p50 * 1e3 / max(iters_max_step, 1.0), 2),
+                  "ms_p50": round(p50, 4), "iters_max_per_step_mean": round(float(lock_iters_max), 2),
+                  "us_per_ipm_iteration": round(p50 * 1e3 / max(lock_iters_max, 1.0), 2),
                   "hbm_bytes_per_launch": io_bytes,
                   "hbm_frac": round(io_bytes / (p50 * 1e-3) / 1e9 / PEAK_HBM_GBS, 5)}
     if rank == 0:
@@ -355,6 +396,10 @@ def main():
         out = {
             "metric": METRIC, "value": round(total / elapsed, 1), "unit": "solves/s", "n_gpus": world,
             "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4),
+            "mode": args.mode,
+            "lockstep": {"value": round(world * B * K / lock_elapsed, 1),
+                         "ms_per_step": round(lock_elapsed / K * 1e3, 4),
+                         "iters_max_per_step_mean": round(float(lock_iters_max), 2)},
             "ms_per_solve_p50": round(p50, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64",
             "data": DATA[cfg],

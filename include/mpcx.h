@@ -188,6 +188,22 @@ int mpcx_step_dev(mpcx_handle* h, int32_t B, double* d_P, double* d_w0, double* 
                   int32_t flags, double* d_w_out, double* d_f_out, double* d_lam_g, double* d_lam_x,
                   int32_t* d_status, int32_t* d_iters, void* stream);
 
+/* K closed-loop steps in ONE launch: every instance runs its own receding-horizon loop
+ * (solve, plant, shift, warm restart -- exactly the sequence of K mpcx_step_dev calls, with
+ * bit-identical results) without waiting for the other instances between steps; instances
+ * are independent, so this changes no result, only how long the slowest solves hold the
+ * batch.  Arguments as mpcx_step_dev, plus:
+ *   K         number of steps (>= 1)
+ *   d_Pseq    K x B x n_p stage references of every step (row s used from step s >= 1,
+ *             the x0 columns are ignored; row 0 must match d_P) or NULL = d_P's for all
+ *   d_tabseq  K x B x N linear-model schedules per step (row s from step s >= 1) or NULL
+ *   d_status, d_iters  K x B (step-major).
+ * On return d_P / d_w0 / d_lam_g0 / d_lam_x0 hold the state after step K (as after K
+ * mpcx_step_dev calls) and d_w_out / d_f_out / d_lam_g / d_lam_x step K's solution. */
+int mpcx_run_dev(mpcx_handle* h, int32_t B, int32_t K, double* d_P, double* d_w0, double* d_lam_g0, double* d_lam_x0,
+                 int32_t flags, const double* d_Pseq, const int32_t* d_tabseq, double* d_w_out, double* d_f_out,
+                 double* d_lam_g, double* d_lam_x, int32_t* d_status, int32_t* d_iters, void* stream);
+
 /* RK4 + Jacobian sweep over B x N shooting intervals (host pointers).
  *   w      B x n_w decision vectors (interleaved layout)
  *   P      B x n_p parameters

@@ -373,6 +373,34 @@ int mpcx_step_dev(mpcx_handle* h, int32_t B, double* d_P, double* d_w0, double* 
   return 0;
 }
 
+int mpcx_run_dev(mpcx_handle* h, int32_t B, int32_t K, double* d_P, double* d_w0, double* d_lam_g0, double* d_lam_x0,
+                 int32_t flags, const double* d_Pseq, const int32_t* d_tabseq, double* d_w_out, double* d_f_out,
+                 double* d_lam_g, double* d_lam_x, int32_t* d_status, int32_t* d_iters, void* stream) {
+  if (!h || !d_P || !d_w0 || !d_w_out) return fail(MPCX_EINVAL, "null argument");
+  if (B < 0) return fail(MPCX_EINVAL, "B < 0");
+  if (K < 1) return fail(MPCX_EINVAL, "K must be >= 1");
+  if (flags & ~(MPCX_STEP_COLD | MPCX_STEP_PRIMAL_ONLY)) return fail(MPCX_EINVAL, "unknown flags");
+  if (d_tabseq && h->spec.model != MPCX_MODEL_LINEAR) return fail(MPCX_EINVAL, "d_tabseq needs a linear model");
+  if (B == 0) return 0;
+  if (int r = check_model_ready(h, B)) return r;
+  HIPCHK(hipSetDevice(h->spec.device));
+  const bool cold = flags & MPCX_STEP_COLD;
+  const bool duals = !(flags & MPCX_STEP_PRIMAL_ONLY) && (d_lam_g0 || d_lam_x0);
+  mpcx::SolveArgs a = make_args(h, B, d_P, cold ? nullptr : d_w0, (duals && !cold) ? d_lam_g0 : nullptr,
+                                (duals && !cold) ? d_lam_x0 : nullptr, h->d_lbw, h->d_ubw, d_w_out, d_f_out, d_lam_g,
+                                d_lam_x, d_status, d_iters);
+  a.P_next = d_P;
+  a.w0_next = d_w0;
+  a.lam0_next = d_lam_g0;
+  a.lamx0_next = d_lam_x0;
+  a.steps = K;
+  a.warm_next = duals ? 1 : 0;
+  a.Pseq = d_Pseq;
+  a.tabseq = d_tabseq;
+  HIPCHK(mpcx::launch_solve(a, (hipStream_t)stream));
+  return 0;
+}
+
 int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w0, const double* lam_g0,
                      const double* lam_x0, const double* lbw, const double* ubw, double* w_out, double* f_out,
                      double* g_out, double* lam_g, double* lam_x, int32_t* status, int32_t* iters) {

@@ -45,6 +45,12 @@ struct SolveArgs {
   double* w0_next;      // B x nw: solution shifted one interval
   double* lam0_next;    // B x ng or null
   double* lamx0_next;   // B x nw or null
+  // multi-step launches (mpcx_run_dev): `steps` closed-loop steps per instance in one
+  // launch, each instance advancing on its own; status/iters are steps x B.
+  int steps;             // <= 1: a single solve
+  int warm_next;         // steps >= 1 start from shifted multipliers (1) or primal only (0)
+  const double* Pseq;    // steps x B x p_stride stage references per step (x0 part unused) or null
+  const int32_t* tabseq; // steps x B x N linear-model schedule per step or null
 };
 
 // What a stage model reads (a local copy: taking the address of the kernel argument

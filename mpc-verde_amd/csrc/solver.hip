@@ -172,8 +172,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     }
   }
   // bound push (IPOPT bound_push / bound_frac = 1e-2; warm start: warm_start_bound_push)
-  const bool warm = a.warm != 0;
-  const double push = warm ? a.bound_push : kBoundPush, frac = warm ? a.bound_push : kBoundFrac;
+  bool warm = a.warm != 0;
   double lx0[NZ];  // given bound multipliers (zU - zL) of my variables
 #pragma unroll
   for (int i = 0; i < NZ; ++i) lx0[i] = 0.0;
@@ -185,20 +184,27 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       for (int i = 0; i < NU; ++i) lx0[NX + i] = l[iuw<NX, NU>(k, i)];
   }
   double zL[NZ], zU[NZ];
+  // starting point of one solve from z (primal guess) and lx0 (given zU - zL): IPOPT's
+  // bound push and dual initialisation -- shared by the launch start and the warm restarts
+  // of multi-step launches, so both give the same bits
+  auto init_point = [&]() __attribute__((always_inline)) {
+    const double push = warm ? a.bound_push : kBoundPush, frac = warm ? a.bound_push : kBoundFrac;
 #pragma unroll
-  for (int i = 0; i < NZ; ++i) {
-    if (hL[i] && hU[i]) {
-      const double pl = fmin(push * fmax(1.0, fabs(lb[i])), frac * (ub[i] - lb[i]));
-      const double pu = fmin(push * fmax(1.0, fabs(ub[i])), frac * (ub[i] - lb[i]));
-      z[i] = fmin(fmax(z[i], lb[i] + pl), ub[i] - pu);
-    } else if (hL[i]) {
-      z[i] = fmax(z[i], lb[i] + push * fmax(1.0, fabs(lb[i])));
-    } else if (hU[i]) {
-      z[i] = fmin(z[i], ub[i] - push * fmax(1.0, fabs(ub[i])));
+    for (int i = 0; i < NZ; ++i) {
+      if (hL[i] && hU[i]) {
+        const double pl = fmin(push * fmax(1.0, fabs(lb[i])), frac * (ub[i] - lb[i]));
+        const double pu = fmin(push * fmax(1.0, fabs(ub[i])), frac * (ub[i] - lb[i]));
+        z[i] = fmin(fmax(z[i], lb[i] + pl), ub[i] - pu);
+      } else if (hL[i]) {
+        z[i] = fmax(z[i], lb[i] + push * fmax(1.0, fabs(lb[i])));
+      } else if (hU[i]) {
+        z[i] = fmin(z[i], ub[i] - push * fmax(1.0, fabs(ub[i])));
+      }
+      zL[i] = hL[i] ? (warm ? fmax(-lx0[i], a.mult_push) : 1.0) : 0.0;
+      zU[i] = hU[i] ? (warm ? fmax(lx0[i], a.mult_push) : 1.0) : 0.0;
     }
-    zL[i] = hL[i] ? (warm ? fmax(-lx0[i], a.mult_push) : 1.0) : 0.0;
-    zU[i] = hU[i] ? (warm ? fmax(lx0[i], a.mult_push) : 1.0) : 0.0;
-  }
+  };
+  init_point();
   double lam[NX];  // lambda_k: multiplier of g_k (the constraint defining X_k)
 #pragma unroll
   for (int i = 0; i < NX; ++i) lam[i] = (warm && a.lam0 && hasX) ? a.lam0[(size_t)inst * ng + NX * k + i] : 0.0;
@@ -243,7 +249,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   int nfilt = 0, fnext = 0;
   int status = valid ? 2 : 0;
   bool done = !valid;
-  int it = 0;
+  int it = 0;        // iteration of this instance's current solve
+  int its = 0;       // its iteration count when it finished
+  const int K = a.steps > 1 ? a.steps : 1;
+  int step = valid ? 0 : K - 1;  // closed-loop step of this instance (multi-step launches)
   // every per-lane array is defined on every lane (lanes past node N included): no
   // indeterminate values for the optimiser to exploit
   double dz[NZ] = {}, dlam[NX] = {}, dzL[NZ] = {}, dzU[NZ] = {};
@@ -259,7 +268,78 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   int st_ph = 9;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
 #endif
-  for (it = 0; it <= a.max_iter; ++it) {
+  // ---- multi-step launches: the closed-loop step boundary of an instance that finished a
+  //      non-final step -- record it, plant x0 <- F(x0, u0*) on lane 0, shift primal and
+  //      multipliers one node (Casadi/multiple_shooting_casadi.py:271-287, the same values
+  //      the fused epilogue below writes), load the next step's references and schedule,
+  //      and restart the solve exactly as a new launch would from those buffers.
+  auto step_boundary = [&]() __attribute__((always_inline)) {
+    const bool bnd = done && step < K - 1;  // group-uniform
+    if (!__any(bnd)) return;
+    constexpr int NS = NZ + NX + NZ;
+    double own[NS], nxt[NS];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+      own[i] = z[i];
+      own[NZ + NX + i] = (zU[i] - zL[i]) / fs;
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) own[NZ + i] = lam[i] / fs;
+    group_next<G, NS>(own, nxt, xw);
+    if (bnd) {
+      if (k == 0) {
+        if (a.status) a.status[(size_t)step * a.B + inst] = status;
+        if (a.iters) a.iters[(size_t)step * a.B + inst] = its;
+        double zp[NZ], xfp[NX], qp;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) zp[i] = x0[i];
+#pragma unroll
+        for (int i = 0; i < NU; ++i) zp[NX + i] = z[NX + i];
+        Model::value(ma, ctx, zp, xfp, qp);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) x0[i] = xfp[i];
+      }
+      ++step;
+      const double* Pn = a.Pseq ? a.Pseq + ((size_t)step * a.B + inst) * a.p_stride : Pin;
+      ModelArgs mst = ma;
+      if (a.tabseq) {
+        mst.lin.tab = a.tabseq + (size_t)step * a.B * N;
+        mst.lin.per_instance = 1;
+      }
+      Model::load_ctx(mst, inst, Pn, k, hasU, ctx);
+      const bool lastX = (k == N), lastU = (k == N - 1);
+      warm = a.warm_next != 0;
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        z[i] = hasX ? (lastX ? own[i] : nxt[i]) : 0.0;
+        lam[i] = (warm && hasX) ? (lastX ? own[NZ + i] : nxt[NZ + i]) : 0.0;
+        lx0[i] = (warm && hasX && k > 0) ? (lastX ? own[NZ + NX + i] : nxt[NZ + NX + i]) : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        z[NX + i] = hasU ? (lastU ? own[NX + i] : nxt[NX + i]) : 0.0;
+        lx0[NX + i] = (warm && hasU) ? (lastU ? own[NZ + 2 * NX + i] : nxt[NZ + 2 * NX + i]) : 0.0;
+      }
+      init_point();
+      mu = warm ? a.mu_init : 0.1;
+      tau = fmax(kTauMin, 1.0 - mu);
+      fs = 1.0;
+      theta_max = theta_min = 0.0;
+      dw_last = 0.0;
+      nfilt = fnext = 0;
+      status = 2;
+      done = false;
+      it = 0;
+      its = 0;
+    }
+  };
+
+  // every pass is one IPM iteration for the instances still solving; instances that
+  // finished a step of a multi-step launch restart at the top of the next pass.  Bounded:
+  // each step ends after at most max_iter + 1 passes.
+  const long max_pass = (long)K * (a.max_iter + 2);
+  for (long pass = 0; pass <= max_pass; ++pass, ++it) {
+    if (K > 1) step_boundary();
     // ------------------------------------------------------------ evaluation (the only call site)
     sweep();
     if (it == 0) {
@@ -350,16 +430,18 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     if (!done && E0 <= a.tol) {
       done = true;
       status = 0;
+      its = it;
     }
-    if (!done && it == a.max_iter) {
+    if (!done && it >= a.max_iter) {
       done = true;
       status = 2;
+      its = a.max_iter;
     }
 #ifdef MPCX_DEBUG_PRINT
     if (inst == 0 && (k % 64) == 0)
       printf("OPT it=%d k=%d fs=%g Ed=%g Ec=%g E0=%g sd=%g lam1=%g z1=%g\n", it, k, fs, Ed, Ec, E0, sd, lam1, z1);
 #endif
-    if (__all(done)) break;
+    if (__all(done && step == K - 1)) break;
 
     STAMP(1);
     // ------------------------------------------------------------ barrier update
@@ -496,6 +578,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     if (!done && failed) {
       done = true;
       status = 3;
+      its = it;
     }
     riccati_gains<NX, NU>(fac, Kk, kfk);  // all lanes at once
 
@@ -685,6 +768,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     if (!done && !accepted) {
       done = true;
       status = 3;
+      its = it;
     }
 
     STAMP(7);
@@ -749,8 +833,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     }
     if (k == 0) {
       if (a.f_out) a.f_out[inst] = fsum;
-      if (a.status) a.status[inst] = status;
-      if (a.iters) a.iters[inst] = it > a.max_iter ? a.max_iter : it;
+      if (a.status) a.status[(size_t)step * a.B + inst] = status;
+      if (a.iters) a.iters[(size_t)step * a.B + inst] = its;
     }
   }
 

@@ -26,7 +26,7 @@ STATUS = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Maximum_Ite
 # C-ABI entry points (include/mpcx.h) -- checked by tests/test_capi_symbols.py
 EXPORTS = ("mpcx_default_spec", "mpcx_create", "mpcx_destroy", "mpcx_last_error", "mpcx_dims", "mpcx_solve_batch",
            "mpcx_solve_batch_dev", "mpcx_plant_step", "mpcx_shift_dev", "mpcx_rk4_sens", "mpcx_rk4_sens_dev",
-           "mpcx_set_linear_model", "mpcx_set_linear_tab_dev", "mpcx_step_dev")
+           "mpcx_set_linear_model", "mpcx_set_linear_tab_dev", "mpcx_step_dev", "mpcx_run_dev")
 STEP_COLD = 1
 STEP_PRIMAL_ONLY = 2
 
@@ -102,6 +102,8 @@ def load():
     lib.mpcx_set_linear_model.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp, ip, ctypes.c_int32]
     lib.mpcx_set_linear_tab_dev.argtypes = [H, ctypes.c_void_p, ctypes.c_int32]
     lib.mpcx_step_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp]
+    lib.mpcx_run_dev.argtypes = [H, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp,
+                                 vp, vp, vp, vp]
     for name in EXPORTS:
         getattr(lib, name)  # AttributeError if an export is missing
     _lib = lib

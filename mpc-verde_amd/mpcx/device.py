@@ -85,6 +85,33 @@ class DeviceLoop:
         with torch.cuda.stream(self.stream):
             self.P[:, self.solver.ocp.nx:].copy_(refs, non_blocking=True)
 
+    def run(self, K, status_out=None, iters_out=None, Pseq=None, tabseq=None):
+        """K closed-loop steps in ONE launch (mpcx_run_dev): each instance runs its own
+        receding-horizon loop without waiting for the others between steps; the results
+        equal K calls of step() bit for bit.  status_out / iters_out: int32 (K, B) device
+        tensors (or None -> allocated).  Pseq (K, B, n_p) float64 and tabseq (K, B, N) int32
+        device tensors give per-step stage references / linear schedules (row 0 = the
+        current ones).  Returns (status, iters)."""
+        lib = _lib.load()
+        s = ctypes_void(self.stream.cuda_stream)
+        st = status_out if status_out is not None else torch.zeros((K, self.B), dtype=torch.int32, device=self.device)
+        it = iters_out if iters_out is not None else torch.zeros((K, self.B), dtype=torch.int32, device=self.device)
+        assert st.shape == (K, self.B) and it.shape == (K, self.B) and st.dtype == it.dtype == torch.int32
+        if Pseq is not None:
+            assert Pseq.dtype == torch.float64 and Pseq.is_contiguous() and Pseq.shape == (K, self.B, self.P.shape[1])
+        if tabseq is not None:
+            assert tabseq.dtype == torch.int32 and tabseq.is_contiguous() and tabseq.shape[:2] == (K, self.B)
+        flags = _lib.STEP_COLD if self._cold else 0
+        if not self.warm_duals:
+            flags |= _lib.STEP_PRIMAL_ONLY
+        d = self.warm_duals
+        _lib.check(lib.mpcx_run_dev(self.solver._h.ptr, self.B, int(K), _ptr(self.P), _ptr(self.w0),
+                                    _ptr(self.lam0) if d else None, _ptr(self.lamx0) if d else None, flags, _ptr(Pseq),
+                                    _ptr(tabseq), _ptr(self.w), _ptr(self.f), _ptr(self.lam), _ptr(self.lamx), _ptr(st),
+                                    _ptr(it), s))
+        self._cold = False
+        return st, it
+
     def set_schedule(self, tab):
         """Per-step stage schedule of a linear model: tab is a (B, N) int32 device tensor
         of table indices read by the next solves/shifts (mpcx_set_linear_tab_dev; LTV

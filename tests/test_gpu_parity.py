@@ -511,3 +511,110 @@ def test_rk4_sens_ragged_tiles(mpcx):
     for k in ("c", "q", "A", "B", "gq"):
         for b in (5, 42, 79):
             np.testing.assert_array_equal(big[k][b], one[k][0], err_msg=k)
+
+
+# ----------------------------------------------------------------------------- multi-step launches
+def _state(lp):
+    return {n: getattr(lp, n).cpu().numpy() for n in ("P", "w", "w0", "lam", "lam0", "lamx", "lamx0", "f")}
+
+
+@pytest.mark.parametrize("N,B,K,warm_duals", [(20, 200, 6, True), (20, 64, 4, False), (100, 24, 3, True)])
+def test_run_equals_lockstep_steps(mpcx, N, B, K, warm_duals):
+    """mpcx_run_dev (K closed-loop steps in one launch, instances not waiting for each
+    other) == K mpcx_step_dev launches, bit for bit: states, per-step status and iterations."""
+    import torch
+    from mpcx import dist
+    from mpcx.device import DeviceLoop
+
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=N))
+    P0 = dist.config2_inputs(0, B)
+    lock = DeviceLoop(solver, P0, warm_duals=warm_duals)
+    run = DeviceLoop(solver, P0, warm_duals=warm_duals)
+    st_l, it_l = [], []
+    for _ in range(K):
+        lock.step()
+        torch.cuda.synchronize()
+        st_l.append(lock.status.cpu().numpy().copy())
+        it_l.append(lock.iters.cpu().numpy().copy())
+    st_r, it_r = run.run(K)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st_r.cpu().numpy(), np.array(st_l))
+    np.testing.assert_array_equal(it_r.cpu().numpy(), np.array(it_l))
+    a, b = _state(lock), _state(run)
+    for n in a:
+        np.testing.assert_array_equal(b[n], a[n], err_msg=n)
+    # a second multi-step launch continues the same trajectory
+    run.run(2)
+    for _ in range(2):
+        lock.step()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(run.P.cpu().numpy(), lock.P.cpu().numpy())
+
+
+def test_run_tracking_with_stage_reference_sequence(mpcx):
+    """Config-3 tracking: per-step references through Pseq == set_stage_refs + step()."""
+    import torch
+    from mpcx import dist
+    from mpcx.device import DeviceLoop
+
+    N, B, K = 30, 64, 5
+    tau0, P0 = dist.config3_inputs(0, B, N=N)
+    solver = mpcx.nlpsol("t", "mi355x", mpcx.unicycle_tracking(N=N))
+    refs = np.stack([mpcx.ocp.circular_reference(tau0, t, N).reshape(B, -1) for t in range(K)])
+    Pseq = np.zeros((K, B, P0.shape[1]))
+    Pseq[:, :, 3:] = refs
+    lock = DeviceLoop(solver, P0)
+    run = DeviceLoop(solver, P0)
+    dr = torch.from_numpy(refs).cuda()
+    st_l = []
+    for t in range(K):
+        lock.set_stage_refs(dr[t])
+        lock.step()
+        torch.cuda.synchronize()
+        st_l.append(lock.iters.cpu().numpy().copy())
+    _, it_r = run.run(K, Pseq=torch.from_numpy(Pseq).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(it_r.cpu().numpy(), np.array(st_l))
+    a, b = _state(lock), _state(run)
+    for n in ("w", "w0", "lam0", "lamx0", "f"):
+        np.testing.assert_array_equal(b[n], a[n], err_msg=n)
+    np.testing.assert_array_equal(b["P"][:, 0:3], a["P"][:, 0:3])  # x0 (run keeps step-0 refs in P)
+
+
+def test_run_ltv_with_schedule_sequence(mpcx):
+    """Config-4 LTV: per-step references (Pseq) and schedules (tabseq) == the lock-step loop."""
+    import torch
+    from mpcx import dist
+    from mpcx.device import DeviceLoop
+
+    N, B, K = 20, 16, 4
+    t0, x0, par = dist.config4_inputs(0, B, N=N)
+    _, _, vref = dist.lane_change()
+    lin = mpcx.lateral_ltv(N=N, Delta=0.05, vref=vref, per_instance_tab=t0)
+    solver = mpcx.nlpsol("ltv", "mi355x", lin)
+    tt = np.minimum(t0[None, :] + np.arange(K)[:, None], 499)
+    refs = np.ascontiguousarray(par[tt].reshape(K, B, -1))
+    tabs = np.ascontiguousarray(np.repeat(tt[:, :, None], N, axis=2).astype(np.int32))
+    P0 = lin.params(x0, par[tt[0]])
+    Pseq = np.zeros((K, B, P0.shape[1]))
+    Pseq[:, :, 4:] = refs
+    dr, dt = torch.from_numpy(refs).cuda(), torch.from_numpy(tabs).cuda()
+    lock = DeviceLoop(solver, P0)
+    it_l = []
+    for t in range(K):
+        lock.set_stage_refs(dr[t])
+        lock.set_schedule(dt[t])
+        lock.step()
+        torch.cuda.synchronize()
+        it_l.append(lock.iters.cpu().numpy().copy())
+    a = _state(lock)
+    run = DeviceLoop(solver, P0)
+    run.set_schedule(dt[0])
+    _, it_r = run.run(K, Pseq=torch.from_numpy(Pseq).cuda(), tabseq=dt)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(it_r.cpu().numpy(), np.array(it_l))
+    b = _state(run)
+    for n in ("w", "w0", "lam0", "lamx0", "f"):
+        np.testing.assert_array_equal(b[n], a[n], err_msg=n)
+    np.testing.assert_array_equal(b["P"][:, 0:4], a["P"][:, 0:4])
+    run.set_schedule(None)
