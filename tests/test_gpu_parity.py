@@ -618,3 +618,21 @@ def test_run_ltv_with_schedule_sequence(mpcx):
         np.testing.assert_array_equal(b[n], a[n], err_msg=n)
     np.testing.assert_array_equal(b["P"][:, 0:4], a["P"][:, 0:4])
     run.set_schedule(None)
+
+
+def test_nonfinite_instance_fails_alone(mpcx):
+    """An instance with a NaN parameter ends with status 3 (IPOPT would report a failure)
+    and leaves every other instance -- including its wave-mate -- bit-identical."""
+    from mpcx import dist
+
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=20))
+    P = dist.config2_inputs(0, 8)
+    ref = solver.solve_batch(P)
+    Pn = P.copy()
+    Pn[3, 1] = np.nan  # instance 3 shares a wave with instance 2 (G = 32)
+    r = solver.solve_batch(Pn)
+    assert r["status"][3] == 3
+    others = [b for b in range(8) if b != 3]
+    np.testing.assert_array_equal(r["status"][others], ref["status"][others])
+    np.testing.assert_array_equal(r["w"][others], ref["w"][others])
+    np.testing.assert_array_equal(r["iters"][others], ref["iters"][others])
