@@ -231,8 +231,9 @@ def main():
     rank, world, local = mdist.env()
     import torch
 
+    local = mdist.device_index(local)
     torch.cuda.set_device(local)
-    mdist.init("nccl")
+    mdist.init(mdist.backend("nccl"))
     import mpcx
     from mpcx.device import DeviceLoop
 

@@ -23,6 +23,25 @@ def env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def device_index(local_rank: int) -> int:
+    """GPU of this rank: LOCAL_RANK, or MPCX_FORCE_DEVICE (test rehearsal of the multi-rank
+    path with several ranks on one GPU; never set in production runs)."""
+    forced = os.environ.get("MPCX_FORCE_DEVICE")
+    return int(forced) if forced is not None else local_rank
+
+
+def backend(default: str = "nccl") -> str:
+    """Process-group backend: RCCL ("nccl") unless MPCX_DIST_BACKEND overrides it (gloo for
+    the one-GPU rehearsal above: RCCL needs a distinct GPU per rank)."""
+    return os.environ.get("MPCX_DIST_BACKEND", default)
+
+
+def _coll_device(device):
+    import torch.distributed as dist
+
+    return None if dist.get_backend() == "gloo" else device
+
+
 def init(backend: str):
     import torch.distributed as dist
 
@@ -148,6 +167,7 @@ def all_gather_stats(S_local, device=None):
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return np.asarray(S_local)
     t = torch.as_tensor(np.ascontiguousarray(S_local), dtype=torch.float64)
+    device = _coll_device(device)
     if device is not None:
         t = t.to(device)
     out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
@@ -161,6 +181,6 @@ def max_over_ranks(x: float, device=None):
 
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return float(x)
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

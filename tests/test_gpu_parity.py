@@ -636,3 +636,31 @@ def test_nonfinite_instance_fails_alone(mpcx):
     np.testing.assert_array_equal(r["status"][others], ref["status"][others])
     np.testing.assert_array_equal(r["w"][others], ref["w"][others])
     np.testing.assert_array_equal(r["iters"][others], ref["iters"][others])
+
+
+def test_bench_two_ranks_rehearsal():
+    """The multi-rank bench path end to end (torch.distributed.run, 2 ranks, weak
+    scaling, stats all_gather, max-over-ranks timing), rehearsed on ONE GPU: both ranks on
+    device 0 and gloo collectives (RCCL needs a GPU per rank; the 8-GPU run is the driver's)."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MPCX_FORCE_DEVICE="0", MPCX_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--no-cpu", "--no-roofline"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 prints ONE line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * d["config"]["batch_per_gpu"]
+    assert d["failed_instances"] == 0 and d["value"] > 0 and d["steps"] == 3

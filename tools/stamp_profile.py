@@ -34,21 +34,29 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--N", type=int, default=20)
+    ap.add_argument("--model", choices=("unicycle", "pend"), default="unicycle")
     a = ap.parse_args()
     lib = mpcx._lib.load()
     lib.mpcx_diag_set_stamp_buffer.argtypes = [ctypes.c_void_p]
-    solver = mpcx.nlpsol("stamps", "mi355x", mpcx.unicycle_point_to_point(N=a.N))
-    loop = DeviceLoop(solver, dist.config2_inputs(0, a.batch))
+    if a.model == "pend":
+        lin = mpcx.inverted_pendulum_qp(N=a.N)
+        solver = mpcx.nlpsol("stamps", "mi355x", lin)
+        loop = DeviceLoop(solver, mpcx.lti.pendulum_params(lin, dist.config5_inputs(0, a.batch), 0.0))
+    else:
+        solver = mpcx.nlpsol("stamps", "mi355x", mpcx.unicycle_point_to_point(N=a.N))
+        loop = DeviceLoop(solver, dist.config2_inputs(0, a.batch))
     for _ in range(a.steps):
         loop.step()
-    G = 16 if a.N < 16 else (32 if a.N < 32 else 64)
+    G = 16 if a.N < 16 else 32 if a.N < 32 else 64 if a.N < 64 else 128 if a.N < 128 else 256
     waves = (a.batch * G + 63) // 64
     buf = torch.zeros(waves * 10, dtype=torch.int64, device="cuda")
     assert lib.mpcx_diag_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
     loop.solve()
     torch.cuda.synchronize()
     acc = buf.view(waves, 10).cpu().numpy().astype(float)
-    iters = loop.iters.cpu().numpy().reshape(waves, -1).max(axis=1)
+    it_inst = loop.iters.cpu().numpy()
+    iters = np.array([it_inst[(w * 64) // G] if G >= 64 else it_inst[w * (64 // G):(w + 1) * (64 // G)].max()
+                      for w in range(waves)])
     slow = int(np.argmax(acc.sum(axis=1)))
     tot = acc[slow].sum()
     out = {"iters_slowest_wave": int(iters[slow]), "cycles_slowest_wave": tot,
