@@ -68,6 +68,13 @@ def unicycle_point_to_point(N=10, T=0.2, M=4, v_max=1.0, omega_max=math.pi / 4, 
                formulation=formulation)
 
 
+def unicycle_point_to_point_mpctools(N=10, T=0.2):
+    """``mpctools/multiple_shooting_mpctools.py:9-70`` (writes ``Casadi/3exemplo.xlsx``): RK4
+    M=1 model, node cost (x - goal)^T diag(1,5,0.1) (x - goal) + u^T u (the script's R is not
+    used by its lfunc, :57-58), |v| <= 1, |w| <= pi/4; p = [x0; goal]."""
+    return OCP(N=N, T=T, M=1, Q=(1.0, 5.0, 0.1), R=(1.0, 1.0), cost="node")
+
+
 def unicycle_tracking(N=10, T=0.2):
     """``Trajectory Tracking/Trajectory_tracking.py:15-72``: RK4 with M=1, node cost
     l(x,u,p_k) with Q=diag(1,1,0.1), R=diag(0.5,0.05), per-stage reference

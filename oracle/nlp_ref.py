@@ -556,3 +556,46 @@ def lq_solve(x0, A, B, c, W, tab, zr, lbu, ubu, x_lb=None, x_ub=None, tol=1e-13)
     X = fx + np.einsum("kij,j->ki", Sx, u)
     J = 0.5 * u @ H @ u + g0 @ u + const
     return X, u.reshape(N, nu), J
+
+
+# ----------------------------------------------------------------------------
+# mpctools point-to-point variant (mpctools/multiple_shooting_mpctools.py -> Casadi/3exemplo.xlsx)
+# ----------------------------------------------------------------------------
+
+
+def mpctools_point_to_point_ocp(N=10):
+    """``mpctools/multiple_shooting_mpctools.py:9-70``: RK4 M=1 model (:51), node cost
+    l = (x - goal)^T Q (x - goal) + u^T u (:57-58: R = I, the script's R is unused)."""
+    return UnicycleOCP(N=N, T=0.2, M=1, Q=(1.0, 5.0, 0.1), R=(1.0, 1.0), cost="node")
+
+
+def unicycle_flow(x, u, T):
+    """Exact flow of the unicycle ODE over T with constant (v, w) -- what the script's
+    plant ``mpc.DiscreteSimulator(ode, Delta)`` (:48, an ODE integrator) computes."""
+    x = np.asarray(x, float)
+    v, w = float(u[0]), float(u[1])
+    th = x[2]
+    if abs(w) < 1e-12:
+        return np.array([x[0] + v * T * np.cos(th), x[1] + v * T * np.sin(th), th])
+    return np.array([x[0] + v / w * (np.sin(th + w * T) - np.sin(th)),
+                     x[1] - v / w * (np.cos(th + w * T) - np.cos(th)), th + w * T])
+
+
+def mpctools_closed_loop(solve_u0_x1, nsim=150, T=0.2, goal=(10.0, 10.0, 0.0)):
+    """``:74-104``: stop when the simulated state is within 0.1 of the goal; each solve
+    starts from the model's own prediction X_1 of the previous solve (``fixvar("x", 0,
+    var["x", 1])``, :94), the logged state is the plant's.  solve_u0_x1(x0) -> (u0, X1).
+    Returns (x (t, 3) logged states, u (t, 2))."""
+    goal = np.asarray(goal)
+    x_sim = [np.zeros(3)]
+    x_solver = np.zeros(3)
+    us = []
+    for t in range(nsim):
+        if np.linalg.norm(x_sim[t] - goal) < 1e-1:
+            break
+        u0, x1 = solve_u0_x1(x_solver)
+        us.append(u0)
+        x_solver = x1
+        x_sim.append(unicycle_flow(x_sim[t], u0, T))
+    n = len(us)
+    return np.array(x_sim[:n]), np.array(us)

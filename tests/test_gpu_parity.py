@@ -664,3 +664,24 @@ def test_bench_two_ranks_rehearsal():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * d["config"]["batch_per_gpu"]
     assert d["failed_instances"] == 0 and d["value"] > 0 and d["steps"] == 3
+
+
+def test_mpctools_variant_closed_loop_3exemplo(mpcx, R, golden):
+    """mpctools/multiple_shooting_mpctools.py on the GPU (node cost, RK4 M=1, R = I): each
+    solve starts from the previous prediction X_1, the plant is the exact ODE flow; the
+    recorded controls of Casadi/3exemplo.xlsx are reproduced and the loop stops at row 88."""
+    rows = np.array(golden["mpctools"]["rows"])
+    ocp = mpcx.unicycle_point_to_point_mpctools(N=10)
+    solver = mpcx.nlpsol("s", "mi355x", ocp)
+    goal = np.array([10.0, 10.0, 0.0])
+
+    def solve(x0):
+        r = solver.solve_batch(np.concatenate([x0, goal])[None])
+        assert r["status"][0] == 0
+        w = r["w"][0]
+        return w[3:5].copy(), w[5:8].copy()
+
+    xs, us = R.mpctools_closed_loop(solve)
+    assert us.shape[0] == rows.shape[0]
+    assert rel_err(us, rows[:, 3:5]) <= REL_TOL
+    assert np.abs(xs - rows[:, 0:3]).max() <= 1e-4

@@ -169,3 +169,29 @@ def test_oracle_fixtures_regenerate():
     assert ok.all()
     np.testing.assert_allclose(W, fx["w"][idx], rtol=0, atol=1e-9)
     np.testing.assert_allclose(J, fx["J"][idx], rtol=1e-12)
+
+
+def test_mpctools_variant_reproduces_3exemplo(golden):
+    """Casadi/3exemplo.xlsx (mpctools/multiple_shooting_mpctools.py): the node-cost, RK4 M=1
+    path that the tracking variant also uses.  The oracle's solves reproduce all recorded
+    controls, the exact-flow plant all recorded states, and the loop stops where it did."""
+    rows = np.array(golden["mpctools"]["rows"])
+    ocp = R.mpctools_point_to_point_ocp()
+    goal = np.array([10.0, 10.0, 0.0])
+
+    def solve(x0):
+        w, info = R.solve_ms(np.concatenate([x0, goal]), ocp)
+        assert info["status"] == "converged"
+        X, U = R.split_w(w, ocp.N)
+        return U[0], X[1]
+
+    xs, us = R.mpctools_closed_loop(solve)
+    assert xs.shape == (rows.shape[0], 3)
+    assert np.abs(us - rows[:, 3:5]).max() <= 5e-7 * np.abs(rows[:, 3:5]).max()
+    # the script's plant is an ODE integrator (CVODES, tolerance ~1e-7 per step): every recorded
+    # transition is the exact flow to 1e-6, and the whole trajectory stays within 5e-5
+    steps = [np.abs(R.unicycle_flow(rows[t, 0:3], rows[t, 3:5], 0.2) - rows[t + 1, 0:3]).max()
+             for t in range(rows.shape[0] - 1)]
+    assert max(steps) <= 1e-6
+    assert np.abs(xs - rows[:, 0:3]).max() <= 5e-5
+    np.testing.assert_allclose(rows[:, 5], 0.2 * np.arange(rows.shape[0]), atol=1e-12)
