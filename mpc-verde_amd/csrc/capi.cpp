@@ -165,7 +165,7 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
     return fail(MPCX_EINVAL, "linear model: (nx, nu) must be (4, 1) or (5, 1)");
   if (s->N < 1 || s->N > 255) return fail(MPCX_EINVAL, "N must be in [1, 255]");
   if (s->M < 1 || s->M > 64) return fail(MPCX_EINVAL, "M must be in [1, 64]");
-  if (!(s->T > 0)) return fail(MPCX_EINVAL, "T must be > 0");
+  if (s->model == MPCX_MODEL_UNICYCLE && !(s->T > 0)) return fail(MPCX_EINVAL, "T must be > 0");
   if (s->cost != MPCX_COST_QUADRATURE && s->cost != MPCX_COST_NODE) return fail(MPCX_EINVAL, "unknown cost");
   if (s->param_layout != MPCX_P_X0_XREF && s->param_layout != MPCX_P_X0_STAGEREF)
     return fail(MPCX_EINVAL, "unknown param_layout");

@@ -425,6 +425,65 @@ def kkt_residual_ms(w, lam_g, P, ocp, pstage=None):
     return float(np.max(np.abs(pg))), float(np.max(np.abs(gval)))
 
 
+def box_qp(H, g0, lb, ub, tol=1e-12, max_iter=500):
+    """min 1/2 u^T H u + g0^T u  s.t.  lb <= u <= ub, H symmetric positive definite.
+
+    Primal active-set method (Nocedal & Wright 2006, Alg. 16.3) on simple bounds: finite
+    termination for strictly convex QPs; the returned point is checked against the KKT
+    conditions (raises if they do not hold)."""
+    n = len(g0)
+    lb = np.asarray(lb, float)
+    ub = np.asarray(ub, float)
+    u = np.clip(np.linalg.solve(H, -g0), lb, ub)
+    W = {}  # index -> -1 (at lb) / +1 (at ub)
+    for i in range(n):
+        if u[i] <= lb[i]:
+            W[i] = -1
+        elif u[i] >= ub[i]:
+            W[i] = 1
+    full = False  # the last step was a full Newton step on the current working set
+    for _ in range(max_iter):
+        g = H @ u + g0
+        fr = np.array([i not in W for i in range(n)])
+        p = np.zeros(n)
+        if fr.any() and not full:
+            p[fr] = np.linalg.solve(H[np.ix_(fr, fr)], -g[fr])
+        # after a full step the equality-constrained subproblem is solved (what a new step
+        # would add is rounding noise, which matters on badly scaled condensed Hessians)
+        if full or np.max(np.abs(p)) <= tol * max(1.0, np.max(np.abs(u))):
+            full = False
+            # multipliers of the working bounds: g_i >= 0 at lb, g_i <= 0 at ub
+            mult = {i: (g[i] if side < 0 else -g[i]) for i, side in W.items()}
+            if not mult or min(mult.values()) >= -tol * max(1.0, np.max(np.abs(g))):
+                break
+            W.pop(min(mult, key=mult.get))
+            continue
+        alpha, block = 1.0, None
+        for i in np.flatnonzero(fr):
+            if p[i] < 0 and lb[i] > -np.inf:
+                a = (lb[i] - u[i]) / p[i]
+                if a < alpha:
+                    alpha, block = a, (i, -1)
+            elif p[i] > 0 and ub[i] < np.inf:
+                a = (ub[i] - u[i]) / p[i]
+                if a < alpha:
+                    alpha, block = a, (i, 1)
+        u = u + alpha * p
+        full = block is None
+        if block is not None:
+            i, side = block
+            u[i] = lb[i] if side < 0 else ub[i]
+            W[i] = side
+    else:
+        raise RuntimeError("box_qp: no convergence")
+    g = H @ u + g0
+    scale = max(1.0, np.max(np.abs(g0)), np.max(np.abs(H)) * max(1.0, np.max(np.abs(u))))
+    kkt = np.where(u <= lb, np.minimum(g, 0.0), np.where(u >= ub, np.maximum(g, 0.0), g))
+    if np.max(np.abs(kkt)) > 1e-9 * scale:
+        raise RuntimeError(f"box_qp: KKT residual {np.max(np.abs(kkt)):.3e}")
+    return u
+
+
 # ----------------------------------------------------------------------------
 # LTI cart-pole QP with move blocking (config 5 family)
 # Inverted_pendulum/inverted_pendulum_single_shooting_mpctools.py:15-78
@@ -448,7 +507,7 @@ def pendulum_qp_solve(x0, A, Bd, N=50, n_free=5, uprev=0.0, umax=200.0, xt=(10.0
                       r=0.01, tol=1e-12):
     """The per-step QP of :34-64 condensed onto the n_free free moves (u_k = u_{n_free-1}
     for k >= n_free, Du = 0 there, :32-42): min sum_{k<N} (q1(x1-xt1))^2 + (q3 x3)^2 + (r Du_k)^2
-    with |u| <= umax, Du_0 = u_0 - uprev.  Exact projected-Newton solve (convex QP).
+    with |u| <= umax, Du_0 = u_0 - uprev.  Exact active-set solve (convex QP).
     Returns u (n_free,)."""
     x0 = np.asarray(x0, float)
     # x_k = A^k x0 + S_k u over the free moves u; u_k = E_k u (E_k selects move min(k, n_free-1))
@@ -476,21 +535,7 @@ def pendulum_qp_solve(x0, A, Bd, N=50, n_free=5, uprev=0.0, umax=200.0, xt=(10.0
     c = np.array(cs)
     H = 2 * Rm.T @ Rm
     g0 = 2 * Rm.T @ c
-    lb, ub = -umax * np.ones(n_free), umax * np.ones(n_free)
-    u = np.clip(np.linalg.solve(H, -g0), lb, ub)
-    for _ in range(100):
-        g = H @ u + g0
-        act = ((u <= lb) & (g > 0)) | ((u >= ub) & (g < 0))
-        fr = ~act
-        un = u.copy()
-        if fr.any():
-            un[fr] = np.linalg.solve(H[np.ix_(fr, fr)], -(g0[fr] + H[np.ix_(fr, act)] @ u[act]))
-        un = np.clip(un, lb, ub)
-        if np.max(np.abs(un - u)) <= tol * max(1.0, np.max(np.abs(u))):
-            u = un
-            break
-        u = un
-    return u
+    return box_qp(H, g0, -umax * np.ones(n_free), umax * np.ones(n_free), tol=tol)
 
 
 def pendulum_closed_loop(nsim=1000, T=0.01, N=50):
@@ -510,7 +555,7 @@ def pendulum_closed_loop(nsim=1000, T=0.01, N=50):
 def lq_solve(x0, A, B, c, W, tab, zr, lbu, ubu, x_lb=None, x_ub=None, tol=1e-13):
     """Generic table-driven linear-quadratic OCP (the model of mpcx MPCX_MODEL_LINEAR):
     x_{k+1} = A_j x_k + B_j u_k + c_j, J = sum_k (z_k - zr_k)^T W_j (z_k - zr_k), j = tab[k],
-    lbu <= u_k <= ubu, condensed onto U and solved exactly by projected Newton.
+    lbu <= u_k <= ubu, condensed onto U and solved exactly by a primal active-set method.
     State bounds are not supported here (use x_lb/x_ub = None).  Returns (X (N+1,nx), U (N,nu), J)."""
     x0 = np.asarray(x0, float)
     N = len(tab)
@@ -540,19 +585,7 @@ def lq_solve(x0, A, B, c, W, tab, zr, lbu, ubu, x_lb=None, x_ub=None, tol=1e-13)
         const += fz @ W[j] @ fz
     lb = np.tile(np.asarray(lbu, float), N)
     ub = np.tile(np.asarray(ubu, float), N)
-    u = np.clip(np.linalg.solve(H, -g0), lb, ub)
-    for _ in range(200):
-        g = H @ u + g0
-        act = ((u <= lb) & (g > 0)) | ((u >= ub) & (g < 0))
-        fr = ~act
-        un = u.copy()
-        if fr.any():
-            un[fr] = np.linalg.solve(H[np.ix_(fr, fr)], -(g0[fr] + H[np.ix_(fr, act)] @ u[act]))
-        un = np.clip(un, lb, ub)
-        if np.max(np.abs(un - u)) <= tol * max(1.0, np.max(np.abs(u))):
-            u = un
-            break
-        u = un
+    u = box_qp(H, g0, lb, ub, tol=tol)
     X = fx + np.einsum("kij,j->ki", Sx, u)
     J = 0.5 * u @ H @ u + g0 @ u + const
     return X, u.reshape(N, nu), J

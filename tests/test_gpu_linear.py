@@ -259,3 +259,44 @@ def test_ltv_device_loop_with_device_schedule(mpcx, R):
             x[b] = lin.A[j] @ x[b] + lin.B[j][:, 0] * u0[b]
         np.testing.assert_allclose(loop.P.cpu().numpy()[:, 0:4], x, rtol=1e-12, atol=1e-12)
     loop.set_schedule(None)
+
+
+@pytest.mark.parametrize("nx,seed", [(4, 0), (4, 1), (5, 2), (5, 3)])
+def test_random_linear_problems_vs_lq_oracle(mpcx, R, nx, seed):
+    """Random LTV problems through the generic linear path: 3 tables of random stable A
+    (spectral radius 0.95), random B, c, SPD stage weights, per-instance random schedules,
+    random per-stage references, |u| <= 1 so that bounds are active; N = 12 and 40.
+    Random problems include degenerate bounds (multiplier ~ 0 at an active bound), where an
+    interior-point solution at tol 1e-8 is O(sqrt(mu)) from the vertex -- as IPOPT's would be:
+    inputs are held to the north-star 1e-4, the objective (first-order insensitive there) to
+    1e-7 relative."""
+    from mpcx import lti
+
+    rng = np.random.default_rng(seed)
+    nu, n_tab, B = 1, 3, 48
+    nz = nx + nu
+    As, Bs, cs, Ws = [], [], [], []
+    for _ in range(n_tab):
+        A = rng.normal(size=(nx, nx))
+        As.append(0.95 * A / max(abs(np.linalg.eigvals(A))))
+        Bs.append(rng.normal(size=(nx, nu)))
+        cs.append(0.1 * rng.normal(size=nx))
+        M = rng.normal(size=(nz, nz))
+        Ws.append(M @ M.T / nz + 0.1 * np.eye(nz))
+    for N in (12, 40):
+        tab = rng.integers(0, n_tab, size=(B, N)).astype(np.int32)
+        lin = lti.LinearOCP(N=N, A=np.stack(As), B=np.stack(Bs), c=np.stack(cs), W=np.stack(Ws), tab=tab,
+                            u_lb=(-1.0,), u_ub=(1.0,))
+        S = mpcx.nlpsol("rnd", "mi355x", lin, {"ipopt": {"max_iter": 500}})
+        x0 = 3.0 * rng.normal(size=(B, nx))
+        zr = rng.normal(size=(B, N, nz))
+        r = S.solve_batch(lin.params(x0, zr))
+        assert np.all(r["status"] == 0), np.unique(r["status"], return_counts=True)
+        U = U_of(r["w"], nx, nu, N)[..., 0]
+        n_active = 0
+        for b in range(B):
+            _, U_ref, J = R.lq_solve(x0[b], lin.A, lin.B, lin.c, lin.W, tab[b], zr[b], [-1.0], [1.0])
+            assert rel(U[b], U_ref[:, 0]) <= 1e-4, (N, b)
+            assert abs(r["f"][b] - J) <= 1e-7 * max(1.0, abs(J)), (N, b)
+            n_active += int(np.any(np.abs(U_ref) >= 1 - 1e-9))
+        assert n_active >= B // 4  # the bounds matter

@@ -107,3 +107,32 @@ def test_linear_to_spec():
     assert (s.lbu[0], s.ubu[0]) == (-200.0, 200.0)
     assert s.lbx[0] == -1e20 and s.ubx[4] == 1e20
     assert lin.n_p == 5 + 6 * 50
+
+
+def test_box_qp_matches_active_set_enumeration():
+    """oracle.box_qp (the LQ oracles' QP solve) vs brute force over all 3^n active sets."""
+    import itertools
+
+    from oracle import nlp_ref as R
+
+    rng = np.random.default_rng(7)
+    for trial in range(20):
+        n = 6
+        M = rng.normal(size=(n, n))
+        H = M @ M.T + 0.05 * np.eye(n)
+        g0 = 3.0 * rng.normal(size=n)
+        lb, ub = -np.ones(n), np.ones(n)
+        u = R.box_qp(H, g0, lb, ub)
+        best = None
+        for sides in itertools.product((-1, 0, 1), repeat=n):
+            s = np.array(sides)
+            fr = s == 0
+            v = np.where(s < 0, lb, np.where(s > 0, ub, 0.0))
+            if fr.any():
+                v[fr] = np.linalg.solve(H[np.ix_(fr, fr)], -(g0[fr] + H[np.ix_(fr, ~fr)] @ v[~fr]))
+            if np.any(v < lb - 1e-12) or np.any(v > ub + 1e-12):
+                continue
+            f = 0.5 * v @ H @ v + g0 @ v
+            if best is None or f < best[0]:
+                best = (f, v)
+        np.testing.assert_allclose(u, best[1], rtol=0, atol=1e-9, err_msg=str(trial))
