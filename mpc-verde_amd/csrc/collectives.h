@@ -118,6 +118,14 @@ __device__ __forceinline__ double gmin(double v, XWave<G>& xw) {
 __device__ __forceinline__ double from_next(double v) { return dpp<kWaveShl1>(v); }
 __device__ __forceinline__ double from_prev(double v) { return dpp<kWaveShr1>(v); }
 
+// value of lane `src` of the wave (any lane; ds_bpermute through the LDS crossbar, no LDS memory)
+__device__ __forceinline__ double from_lane(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b & 0xffffffffLL));
+  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // out[i] = v[i] of node k+1 for node-parallel phases; for multi-wave groups lane 63 of
 // wave w receives lane 0 of wave w+1 through LDS.
 template <int G, int n>

@@ -619,12 +619,57 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         }
       };
       if constexpr (G <= 64) {
-        for (int j = 0; j <= N; ++j) {
-          double dxi[NX];
+        // dx_k = T_{k-1}( ... T_0(c0)) with affine T_j(x) = Acl_j x + ccl_j: an inclusive
+        // parallel prefix of map compositions (Hillis-Steele, log2 G levels, all lanes busy)
+        // instead of N+1 dependent steps.  Lane k starts with T_{k-1} (lane 0: the constant
+        // map c0) and composes with the partial map of lane k-d at each level.
+        constexpr int NM = NX * NX + NX;
+        double Am[NX * NX], cm[NX];
+        {
+          double own[NM], prv[NM];
 #pragma unroll
-          for (int i = 0; i < NX; ++i) dxi[i] = from_prev(dxn[i]);
-          if (k == j) fwd_node(dxi);
+          for (int i = 0; i < NX * NX; ++i) own[i] = Acl[i];
+#pragma unroll
+          for (int i = 0; i < NX; ++i) own[NX * NX + i] = ccl[i];
+#pragma unroll
+          for (int i = 0; i < NM; ++i) prv[i] = from_prev(own[i]);
+#pragma unroll
+          for (int i = 0; i < NX * NX; ++i) Am[i] = (k == 0) ? 0.0 : prv[i];
+#pragma unroll
+          for (int i = 0; i < NX; ++i) cm[i] = (k == 0) ? c0[i] : prv[NX * NX + i];
         }
+#pragma unroll
+        for (int d = 1; d < G; d <<= 1) {
+          const int src = (lane - d) & 63;
+          double Ao[NX * NX], co[NX];
+#pragma unroll
+          for (int i = 0; i < NX * NX; ++i) Ao[i] = from_lane(Am[i], src);
+#pragma unroll
+          for (int i = 0; i < NX; ++i) co[i] = from_lane(cm[i], src);
+          if (k >= d) {  // compose: (Am, cm) o (Ao, co)
+            double An[NX * NX], cn[NX];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+              double acc = cm[r];
+#pragma unroll
+              for (int m = 0; m < NX; ++m) acc = fma(Am[r * NX + m], co[m], acc);
+              cn[r] = acc;
+#pragma unroll
+              for (int c = 0; c < NX; ++c) {
+                double e = Am[r * NX] * Ao[c];
+#pragma unroll
+                for (int m = 1; m < NX; ++m) e = fma(Am[r * NX + m], Ao[m * NX + c], e);
+                An[r * NX + c] = e;
+              }
+            }
+#pragma unroll
+            for (int i = 0; i < NX * NX; ++i) Am[i] = An[i];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) cm[i] = cn[i];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dz[i] = cm[i];
       } else {  // wave by wave from node 0; the state step crosses waves through LDS
         const int wv = (int)(threadIdx.x >> 6);
         for (int ph = 0; ph < XWave<G>::W; ++ph) {
