@@ -473,15 +473,16 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     for (int i = 0; i < NZ; ++i) {
       sig[i] = 0;
       gp[i] = gq[i];
+      // one rcp64 per slack instead of IEEE divisions (each a ~10-instruction sequence)
       if (hL[i]) {
-        const double s = z[i] - lb[i];
-        sig[i] += zL[i] / s;
-        gp[i] -= mu / s;
+        const double rs = rcp64(z[i] - lb[i]);
+        sig[i] = fma(zL[i], rs, sig[i]);
+        gp[i] = fma(-mu, rs, gp[i]);
       }
       if (hU[i]) {
-        const double s = ub[i] - z[i];
-        sig[i] += zU[i] / s;
-        gp[i] += mu / s;
+        const double rs = rcp64(ub[i] - z[i]);
+        sig[i] = fma(zU[i], rs, sig[i]);
+        gp[i] = fma(mu, rs, gp[i]);
       }
     }
 
@@ -723,21 +724,22 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
     for (int i = 0; i < NZ; ++i) {
       dzL[i] = dzU[i] = 0.0;
+      const double rdz = rcp64(dz[i]);
       if (hL[i]) {
-        const double s = z[i] - lb[i];
-        dzL[i] = mu / s - zL[i] - zL[i] / s * dz[i];
-        if (dz[i] < 0) amax_l = fmin(amax_l, -tau * s / dz[i]);
-        if (dzL[i] < 0) az_l = fmin(az_l, -tau * zL[i] / dzL[i]);
+        const double s = z[i] - lb[i], rs = rcp64(s);
+        dzL[i] = fma(mu, rs, -zL[i]) - zL[i] * rs * dz[i];
+        if (dz[i] < 0) amax_l = fmin(amax_l, -tau * s * rdz);
+        if (dzL[i] < 0) az_l = fmin(az_l, -tau * zL[i] * rcp64(dzL[i]));
       }
       if (hU[i]) {
-        const double s = ub[i] - z[i];
-        dzU[i] = mu / s - zU[i] + zU[i] / s * dz[i];
-        if (dz[i] > 0) amax_l = fmin(amax_l, tau * s / dz[i]);
-        if (dzU[i] < 0) az_l = fmin(az_l, -tau * zU[i] / dzU[i]);
+        const double s = ub[i] - z[i], rs = rcp64(s);
+        dzU[i] = fma(mu, rs, -zU[i]) + zU[i] * rs * dz[i];
+        if (dz[i] > 0) amax_l = fmin(amax_l, tau * s * rdz);
+        if (dzU[i] < 0) az_l = fmin(az_l, -tau * zU[i] * rcp64(dzU[i]));
       }
       const bool own = (i < NX) ? hasX : hasU;
       if (own) {
-        tiny_l = fmax(tiny_l, fabs(dz[i]) / (1.0 + fabs(z[i])));
+        tiny_l = fmax(tiny_l, fabs(dz[i]) * rcp64(1.0 + fabs(z[i])));
         gd_l += gp[i] * dz[i];
       }
     }
@@ -834,12 +836,12 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
       for (int i = 0; i < NZ; ++i) {
         if (hL[i]) {
-          const double s = z[i] - lb[i];
-          zL[i] = fmax(fmin(zL[i] + az * dzL[i], kKappaSigma * mu / s), mu / (kKappaSigma * s));
+          const double mrs = mu * rcp64(z[i] - lb[i]);
+          zL[i] = fmax(fmin(zL[i] + az * dzL[i], kKappaSigma * mrs), mrs * (1.0 / kKappaSigma));
         }
         if (hU[i]) {
-          const double s = ub[i] - z[i];
-          zU[i] = fmax(fmin(zU[i] + az * dzU[i], kKappaSigma * mu / s), mu / (kKappaSigma * s));
+          const double mrs = mu * rcp64(ub[i] - z[i]);
+          zU[i] = fmax(fmin(zU[i] + az * dzU[i], kKappaSigma * mrs), mrs * (1.0 / kKappaSigma));
         }
       }
     }
