@@ -759,9 +759,11 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     bool searching = !done && !tinystep;
     bool accepted = !done && tinystep;
     bool ftype = tinystep;
-    // switching-condition powers, loop-invariant over the trials
-    const double pw_th = pow(thk, kSTheta), pw_gd = gd < 0 ? pow(-gd, kSPhi) : 0.0;
-    const double amin = gd < 0 ? kGammaAlpha * fmin(kGammaTheta, fmin(kGammaPhi * thk / (-gd), kDeltaSw * pw_th / pw_gd))
+    // switching condition alpha (-gd)^s_phi > delta theta^s_theta  <=>  alpha > sw_a with
+    // sw_a = delta theta^s_theta / (-gd)^s_phi -- also the third term of alpha_min; one exp of
+    // logs, loop-invariant over the trials
+    const double sw_a = gd < 0 ? exp(log(kDeltaSw) + kSTheta * log(thk) - kSPhi * log(-gd)) : 0.0;
+    const double amin = gd < 0 ? kGammaAlpha * fmin(kGammaTheta, fmin(kGammaPhi * thk / (-gd), sw_a))
                                : kGammaAlpha * kGammaTheta;
     for (int ls = 0; ls < 80; ++ls) {
       if (!__any(searching)) break;
@@ -791,7 +793,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         bool acc = isfinite(pht) && isfinite(tht) && tht <= theta_max && !infilter;
         bool ft = false;
         if (acc) {
-          const bool sw = gd < 0 && alpha * pw_gd > kDeltaSw * pw_th;
+          const bool sw = gd < 0 && alpha > sw_a;
           if (thk <= theta_min && sw) {
             acc = pht - phk <= kEtaPhi * alpha * gd + 10.0 * kEps * fabs(phk);
             ft = acc;
