@@ -102,7 +102,8 @@ __device__ __forceinline__ double barrier_logsum(const double* z, const double* 
 template <class Model, int G>
 __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(SolveArgs a) {
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2, NP = NX * (NX + 1) / 2;
-  static_assert(NP + NX <= kXchStride && 2 * NZ + NX <= kXchStride, "LDS exchange slot too small");
+  static_assert(NP + NX <= kXchStride && 2 * NZ + NX <= kXchStride && NX * NX + NX <= kXchStride,
+                "LDS exchange slot too small");
   const int lane = threadIdx.x & 63;
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int k = (int)(gid & (G - 1));  // node of this lane
@@ -586,9 +587,6 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     STAMP(4);
     // ------------------------------------------------------------ forward sweep: dw (lane k-1 -> k)
     {
-      double dxn[NX];
-#pragma unroll
-      for (int i = 0; i < NX; ++i) dxn[i] = 0.0;
       // closed-loop map of the step, node-parallel (off the sequential chain):
       // dx_{k+1} = (A + B K) dx_k + (c + B k_f);  du_k = k_f + K dx_k afterwards
       double Acl[NX * NX], ccl[NX];
@@ -608,23 +606,17 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           Acl[r * NX + m] = e;
         }
       }
-      auto fwd_node = [&](const double* dxi) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dz[i] = (k == 0) ? c0[i] : dxi[i];
-#pragma unroll
-        for (int r = 0; r < NX; ++r) {
-          double acc = ccl[r];
-#pragma unroll
-          for (int m = 0; m < NX; ++m) acc = fma(Acl[r * NX + m], dz[m], acc);
-          dxn[r] = acc;
-        }
-      };
-      if constexpr (G <= 64) {
+      {
         // dx_k = T_{k-1}( ... T_0(c0)) with affine T_j(x) = Acl_j x + ccl_j: an inclusive
-        // parallel prefix of map compositions (Hillis-Steele, log2 G levels, all lanes busy)
-        // instead of N+1 dependent steps.  Lane k starts with T_{k-1} (lane 0: the constant
-        // map c0) and composes with the partial map of lane k-d at each level.
+        // parallel prefix of map compositions (Hillis-Steele, log2 64 levels per wave, all
+        // lanes busy) instead of N+1 dependent steps.  Lane k starts with T_{k-1} (lane 0:
+        // the constant map c0) and composes with the partial map of lane k-d at each level.
+        // Multi-wave groups scan every wave at once; the first lane of wave w gets
+        // T_{64w-1} from wave w-1 through LDS, and the waves' partial results are chained
+        // by one LDS handoff of dx per wave boundary.
         constexpr int NM = NX * NX + NX;
+        constexpr int GW = G < 64 ? G : 64;  // lanes scanned per wave
+        const int wv = G > 64 ? (int)(threadIdx.x >> 6) : 0;
         double Am[NX * NX], cm[NX];
         {
           double own[NM], prv[NM];
@@ -634,20 +626,31 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           for (int i = 0; i < NX; ++i) own[NX * NX + i] = ccl[i];
 #pragma unroll
           for (int i = 0; i < NM; ++i) prv[i] = from_prev(own[i]);
+          if constexpr (G > 64) {  // lane 0 of wave w > 0: T_{64w-1} lives on lane 63 of wave w-1
+            double* b = xw.cur();
+            if (lane == 63 && wv < XWave<G>::W - 1)
+#pragma unroll
+              for (int i = 0; i < NM; ++i) b[wv * kXchStride + i] = own[i];
+            xw.sync();
+            if (lane == 0 && wv > 0)
+#pragma unroll
+              for (int i = 0; i < NM; ++i) prv[i] = xw.prev()[(wv - 1) * kXchStride + i];
+          }
 #pragma unroll
           for (int i = 0; i < NX * NX; ++i) Am[i] = (k == 0) ? 0.0 : prv[i];
 #pragma unroll
           for (int i = 0; i < NX; ++i) cm[i] = (k == 0) ? c0[i] : prv[NX * NX + i];
         }
+        const int kw = k & (GW - 1);  // position inside the wave
 #pragma unroll
-        for (int d = 1; d < G; d <<= 1) {
+        for (int d = 1; d < GW; d <<= 1) {
           const int src = (lane - d) & 63;
           double Ao[NX * NX], co[NX];
 #pragma unroll
           for (int i = 0; i < NX * NX; ++i) Ao[i] = from_lane(Am[i], src);
 #pragma unroll
           for (int i = 0; i < NX; ++i) co[i] = from_lane(cm[i], src);
-          if (k >= d) {  // compose: (Am, cm) o (Ao, co)
+          if (kw >= d) {  // compose: (Am, cm) o (Ao, co)
             double An[NX * NX], cn[NX];
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -669,30 +672,31 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
             for (int i = 0; i < NX; ++i) cm[i] = cn[i];
           }
         }
+        if constexpr (G > 64) {
+          // wave w's lanes hold maps dx_{64w-1} -> dx_k; chain the waves in order
+          for (int ph = 1; ph < XWave<G>::W; ++ph) {
+            double* b = xw.cur();
+            if (wv == ph - 1 && lane == 63)
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dz[i] = cm[i];
-      } else {  // wave by wave from node 0; the state step crosses waves through LDS
-        const int wv = (int)(threadIdx.x >> 6);
-        for (int ph = 0; ph < XWave<G>::W; ++ph) {
-          if (wv == ph) {
-            const double* in = xw.prev();  // dx of node 64 ph, written by wave ph - 1
-            for (int j = 64 * ph; j <= min(N, 64 * ph + 63); ++j) {
-              double dxi[NX];
+              for (int i = 0; i < NX; ++i) b[i] = cm[i];
+            xw.sync();
+            if (wv == ph) {
+              const double* in = xw.prev();
+              double cn[NX];
 #pragma unroll
-              for (int i = 0; i < NX; ++i) dxi[i] = from_prev(dxn[i]);
-              if (j == 64 * ph && ph > 0 && lane == 0)
+              for (int r = 0; r < NX; ++r) {
+                double acc = cm[r];
 #pragma unroll
-                for (int i = 0; i < NX; ++i) dxi[i] = in[i];
-              if (k == j) fwd_node(dxi);
-            }
-            if (ph < XWave<G>::W - 1 && lane == 63) {
-              double* out = xw.cur();
+                for (int m = 0; m < NX; ++m) acc = fma(Am[r * NX + m], in[m], acc);
+                cn[r] = acc;
+              }
 #pragma unroll
-              for (int i = 0; i < NX; ++i) out[i] = dxn[i];
+              for (int i = 0; i < NX; ++i) cm[i] = cn[i];
             }
           }
-          xw.sync();
         }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dz[i] = cm[i];
       }
       // du_k = k_f + K dx_k on all lanes at once (the last node has no control)
 #pragma unroll
