@@ -28,6 +28,7 @@ struct mpcx_handle {
   double *d_P = nullptr, *d_w0 = nullptr, *d_w = nullptr, *d_f = nullptr, *d_lam = nullptr;
   double *d_lam0 = nullptr, *d_lamx0 = nullptr, *d_lamx = nullptr;
   int32_t *d_status = nullptr, *d_iters = nullptr;
+  double *d_u = nullptr, *d_x = nullptr, *d_q = nullptr, *d_g = nullptr;  // plant / constraint outputs
   size_t cap_sweep = 0;
   double* d_sweep = nullptr;
   // linear model tables (MPCX_MODEL_LINEAR)
@@ -85,30 +86,66 @@ void spec_bounds(const mpcx_spec& s, std::vector<double>& lb, std::vector<double
   }
 }
 
+// Device buffers are released by the helpers below, which also null the pointers: a failed
+// (re)allocation leaves the handle in a clean state (no dangling or half-set buffers).
+template <class T>
+void dev_free(T*& p) {
+  (void)hipFree(p);
+  p = nullptr;
+}
+
+void free_workspace(mpcx_handle* h) {
+  dev_free(h->d_P);
+  dev_free(h->d_w0);
+  dev_free(h->d_w);
+  dev_free(h->d_f);
+  dev_free(h->d_lam);
+  dev_free(h->d_status);
+  dev_free(h->d_iters);
+  dev_free(h->d_lam0);
+  dev_free(h->d_lamx0);
+  dev_free(h->d_lamx);
+  dev_free(h->d_u);
+  dev_free(h->d_x);
+  dev_free(h->d_q);
+  dev_free(h->d_g);
+  h->cap_B = 0;
+}
+
+void free_linear(mpcx_handle* h) {
+  dev_free(h->d_linA);
+  dev_free(h->d_linB);
+  dev_free(h->d_linc);
+  dev_free(h->d_linW);
+  dev_free(h->d_lintab);
+  h->lin_ntab = h->lin_rows = 0;
+  h->ext_tab = nullptr;
+  h->ext_rows = 0;
+}
+
+// per-batch workspace of the host-pointer entry points, grown on demand (never shrunk)
 int ensure(mpcx_handle* h, size_t B) {
   if (B <= h->cap_B) return 0;
-  size_t nb = B < 256 ? 256 : B;
-  (void)hipFree(h->d_P);
-  (void)hipFree(h->d_w0);
-  (void)hipFree(h->d_w);
-  (void)hipFree(h->d_f);
-  (void)hipFree(h->d_lam);
-  (void)hipFree(h->d_status);
-  (void)hipFree(h->d_iters);
-  (void)hipFree(h->d_lam0);
-  (void)hipFree(h->d_lamx0);
-  (void)hipFree(h->d_lamx);
-  h->cap_B = 0;
-  HIPCHK(hipMalloc(&h->d_P, nb * h->np * sizeof(double)));
-  HIPCHK(hipMalloc(&h->d_w0, nb * h->nw * sizeof(double)));
-  HIPCHK(hipMalloc(&h->d_w, nb * h->nw * sizeof(double)));
-  HIPCHK(hipMalloc(&h->d_f, nb * sizeof(double)));
-  HIPCHK(hipMalloc(&h->d_lam, nb * h->ng * sizeof(double)));
-  HIPCHK(hipMalloc(&h->d_status, nb * sizeof(int32_t)));
-  HIPCHK(hipMalloc(&h->d_iters, nb * sizeof(int32_t)));
-  HIPCHK(hipMalloc(&h->d_lam0, nb * h->ng * sizeof(double)));
-  HIPCHK(hipMalloc(&h->d_lamx0, nb * h->nw * sizeof(double)));
-  HIPCHK(hipMalloc(&h->d_lamx, nb * h->nw * sizeof(double)));
+  const size_t nb = B < 256 ? 256 : B;
+  free_workspace(h);
+  const int nx = h->spec.nx, nu = h->spec.nu;
+  struct Buf {
+    void** p;
+    size_t bytes;
+  } bufs[] = {{(void**)&h->d_P, nb * h->np * sizeof(double)},   {(void**)&h->d_w0, nb * h->nw * sizeof(double)},
+              {(void**)&h->d_w, nb * h->nw * sizeof(double)},   {(void**)&h->d_f, nb * sizeof(double)},
+              {(void**)&h->d_lam, nb * h->ng * sizeof(double)}, {(void**)&h->d_status, nb * sizeof(int32_t)},
+              {(void**)&h->d_iters, nb * sizeof(int32_t)},      {(void**)&h->d_lam0, nb * h->ng * sizeof(double)},
+              {(void**)&h->d_lamx0, nb * h->nw * sizeof(double)}, {(void**)&h->d_lamx, nb * h->nw * sizeof(double)},
+              {(void**)&h->d_u, nb * nu * sizeof(double)},      {(void**)&h->d_x, nb * nx * sizeof(double)},
+              {(void**)&h->d_q, nb * sizeof(double)},           {(void**)&h->d_g, nb * h->ng * sizeof(double)}};
+  for (const Buf& b : bufs) {
+    const hipError_t e = hipMalloc(b.p, b.bytes);
+    if (e != hipSuccess) {
+      free_workspace(h);
+      return hipfail(e, "workspace allocation");
+    }
+  }
   h->cap_B = nb;
   return 0;
 }
@@ -212,26 +249,13 @@ void mpcx_destroy(mpcx_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->spec.device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  (void)hipFree(h->d_lbw);
-  (void)hipFree(h->d_ubw);
-  (void)hipFree(h->d_lbw_call);
-  (void)hipFree(h->d_ubw_call);
-  (void)hipFree(h->d_P);
-  (void)hipFree(h->d_w0);
-  (void)hipFree(h->d_w);
-  (void)hipFree(h->d_f);
-  (void)hipFree(h->d_lam);
-  (void)hipFree(h->d_status);
-  (void)hipFree(h->d_iters);
-  (void)hipFree(h->d_lam0);
-  (void)hipFree(h->d_lamx0);
-  (void)hipFree(h->d_lamx);
-  (void)hipFree(h->d_sweep);
-  (void)hipFree(h->d_linA);
-  (void)hipFree(h->d_linB);
-  (void)hipFree(h->d_linc);
-  (void)hipFree(h->d_linW);
-  (void)hipFree(h->d_lintab);
+  dev_free(h->d_lbw);
+  dev_free(h->d_ubw);
+  dev_free(h->d_lbw_call);
+  dev_free(h->d_ubw_call);
+  free_workspace(h);
+  dev_free(h->d_sweep);
+  free_linear(h);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -253,29 +277,33 @@ int mpcx_set_linear_model(mpcx_handle* h, int32_t n_tab, const double* A, const 
   for (long i = 0; i < (long)tab_rows * N; ++i)
     if (tab[i] < 0 || tab[i] >= n_tab) return fail(MPCX_EINVAL, "table index out of range at " + std::to_string(i));
   HIPCHK(hipSetDevice(h->spec.device));
-  (void)hipFree(h->d_linA);
-  (void)hipFree(h->d_linB);
-  (void)hipFree(h->d_linc);
-  (void)hipFree(h->d_linW);
-  (void)hipFree(h->d_lintab);
-  h->d_linA = h->d_linB = h->d_linc = h->d_linW = nullptr;
-  h->d_lintab = nullptr;
-  h->lin_ntab = h->lin_rows = 0;
+  HIPCHK(hipStreamSynchronize(h->stream));  // no launch may still read the old tables
+  free_linear(h);
   std::vector<double> cz((size_t)n_tab * nx, 0.0);
-  HIPCHK(hipMalloc(&h->d_linA, (size_t)n_tab * nx * nx * sizeof(double)));
-  HIPCHK(hipMalloc(&h->d_linB, (size_t)n_tab * nx * nu * sizeof(double)));
-  HIPCHK(hipMalloc(&h->d_linc, (size_t)n_tab * nx * sizeof(double)));
-  HIPCHK(hipMalloc(&h->d_linW, (size_t)n_tab * nh * sizeof(double)));
-  HIPCHK(hipMalloc(&h->d_lintab, (size_t)tab_rows * N * sizeof(int32_t)));
-  HIPCHK(hipMemcpy(h->d_linA, A, (size_t)n_tab * nx * nx * sizeof(double), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->d_linB, B, (size_t)n_tab * nx * nu * sizeof(double), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->d_linc, c ? c : cz.data(), (size_t)n_tab * nx * sizeof(double), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->d_linW, W, (size_t)n_tab * nh * sizeof(double), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->d_lintab, tab, (size_t)tab_rows * N * sizeof(int32_t), hipMemcpyHostToDevice));
+  const hipError_t e = [&]() {
+    hipError_t r;
+    if ((r = hipMalloc(&h->d_linA, (size_t)n_tab * nx * nx * sizeof(double))) != hipSuccess) return r;
+    if ((r = hipMalloc(&h->d_linB, (size_t)n_tab * nx * nu * sizeof(double))) != hipSuccess) return r;
+    if ((r = hipMalloc(&h->d_linc, (size_t)n_tab * nx * sizeof(double))) != hipSuccess) return r;
+    if ((r = hipMalloc(&h->d_linW, (size_t)n_tab * nh * sizeof(double))) != hipSuccess) return r;
+    if ((r = hipMalloc(&h->d_lintab, (size_t)tab_rows * N * sizeof(int32_t))) != hipSuccess) return r;
+    if ((r = hipMemcpy(h->d_linA, A, (size_t)n_tab * nx * nx * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+      return r;
+    if ((r = hipMemcpy(h->d_linB, B, (size_t)n_tab * nx * nu * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+      return r;
+    if ((r = hipMemcpy(h->d_linc, c ? c : cz.data(), (size_t)n_tab * nx * sizeof(double), hipMemcpyHostToDevice)) !=
+        hipSuccess)
+      return r;
+    if ((r = hipMemcpy(h->d_linW, W, (size_t)n_tab * nh * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+      return r;
+    return hipMemcpy(h->d_lintab, tab, (size_t)tab_rows * N * sizeof(int32_t), hipMemcpyHostToDevice);
+  }();
+  if (e != hipSuccess) {
+    free_linear(h);  // never leave a half-set table behind (check_model_ready tests d_linA)
+    return hipfail(e, "mpcx_set_linear_model");
+  }
   h->lin_ntab = n_tab;
   h->lin_rows = tab_rows;
-  h->ext_tab = nullptr;
-  h->ext_rows = 0;
   return 0;
 }
 
@@ -449,15 +477,9 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
   if (iters) HIPCHK(hipMemcpyAsync(iters, h->d_iters, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (g_out) {  // constraint values at the solution (constraints kernel on the device)
-    double* d_g = nullptr;
-    HIPCHK(hipMalloc(&d_g, (size_t)B * h->ng * sizeof(double)));
-    const hipError_t e1 = mpcx::launch_constraints(a, h->d_w, d_g, s);
-    const hipError_t e2 = e1 == hipSuccess ? hipMemcpyAsync(g_out, d_g, (size_t)B * h->ng * sizeof(double),
-                                                            hipMemcpyDeviceToHost, s)
-                                           : e1;
-    const hipError_t e3 = e2 == hipSuccess ? hipStreamSynchronize(s) : e2;
-    (void)hipFree(d_g);
-    HIPCHK(e3);
+    HIPCHK(mpcx::launch_constraints(a, h->d_w, h->d_g, s));
+    HIPCHK(hipMemcpyAsync(g_out, h->d_g, (size_t)B * h->ng * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
   }
   return 0;
 }
@@ -469,11 +491,8 @@ int mpcx_plant_step(mpcx_handle* h, int32_t B, const double* P, const double* u,
   HIPCHK(hipSetDevice(h->spec.device));
   hipStream_t s = h->stream;
   const int nx = h->spec.nx, nu = h->spec.nu;
-  double *dP = nullptr, *dU = nullptr, *dX = nullptr, *dQ = nullptr;
-  HIPCHK(hipMalloc(&dP, (size_t)B * h->np * sizeof(double)));
-  HIPCHK(hipMalloc(&dU, (size_t)B * nu * sizeof(double)));
-  HIPCHK(hipMalloc(&dX, (size_t)B * nx * sizeof(double)));
-  HIPCHK(hipMalloc(&dQ, (size_t)B * sizeof(double)));
+  if (int r = ensure(h, B)) return r;
+  double *dP = h->d_P, *dU = h->d_u, *dX = h->d_x, *dQ = h->d_q;
   HIPCHK(hipMemcpyAsync(dP, P, (size_t)B * h->np * sizeof(double), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(dU, u, (size_t)B * nu * sizeof(double), hipMemcpyHostToDevice, s));
   mpcx::SolveArgs a = make_args(h, B, dP, nullptr, nullptr, nullptr, h->d_lbw, h->d_ubw, nullptr, nullptr, nullptr,
@@ -482,10 +501,6 @@ int mpcx_plant_step(mpcx_handle* h, int32_t B, const double* P, const double* u,
   HIPCHK(hipMemcpyAsync(xf, dX, (size_t)B * nx * sizeof(double), hipMemcpyDeviceToHost, s));
   if (qf) HIPCHK(hipMemcpyAsync(qf, dQ, (size_t)B * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  (void)hipFree(dP);
-  (void)hipFree(dU);
-  (void)hipFree(dX);
-  (void)hipFree(dQ);
   return 0;
 }
 
