@@ -976,14 +976,14 @@ __global__ __launch_bounds__(256) void rk4_sens_kernel(int B, int N, StageParams
     // one 24-field record per stage: c(3) q(1) A(9) B(6) grad q(5) -- a wave's whole
     // output of a stage is one contiguous 12 KB block
 #pragma unroll
-    for (int i = 0; i < 3; ++i) J[tix(k, kRec, i, b, T)] = xf[i] - xn[i];
-    J[tix(k, kRec, 3, b, T)] = q;
+    for (int i = 0; i < 3; ++i) __builtin_nontemporal_store(xf[i] - xn[i], &J[tix(k, kRec, i, b, T)]);
+    __builtin_nontemporal_store(q, &J[tix(k, kRec, 3, b, T)]);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) J[tix(k, kRec, 4 + i, b, T)] = A[i];
+    for (int i = 0; i < 9; ++i) __builtin_nontemporal_store(A[i], &J[tix(k, kRec, 4 + i, b, T)]);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) J[tix(k, kRec, 13 + i, b, T)] = Bm[i];
+    for (int i = 0; i < 6; ++i) __builtin_nontemporal_store(Bm[i], &J[tix(k, kRec, 13 + i, b, T)]);
 #pragma unroll
-    for (int i = 0; i < 5; ++i) J[tix(k, kRec, 19 + i, b, T)] = g[i];
+    for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(g[i], &J[tix(k, kRec, 19 + i, b, T)]);
 #pragma unroll
     for (int i = 0; i < 3; ++i) x[i] = xn[i];
   }

@@ -74,6 +74,28 @@ __global__ void sweep_tiled64(double* __restrict__ o, int B, int S) {
 #pragma unroll
     for (int f = 0; f < 24; ++f) o[(((long)k * (B / 64) + tile) * 24 + f) * 64 + lane] = k + f + b;
 }
+// the sweep's exact traffic without its arithmetic: tiled X/U loads, one 24-field record store
+// per stage (tix layout of solver.hip), 64 instances per tile
+__device__ __forceinline__ size_t ptix(int stage, int F, int i, long b, long T) {
+  return (((size_t)stage * T + (b >> 6)) * F + i) * 64 + (b & 63);
+}
+__global__ void sweep_copy(const double* __restrict__ X, const double* __restrict__ U, double* __restrict__ J, int B,
+                           int S) {
+  const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const long T = (B + 63) / 64;
+  double x0 = X[ptix(0, 3, 0, b, T)], x1 = X[ptix(0, 3, 1, b, T)], x2 = X[ptix(0, 3, 2, b, T)];
+  for (int k = 0; k < S; ++k) {
+    const double n0 = X[ptix(k + 1, 3, 0, b, T)], n1 = X[ptix(k + 1, 3, 1, b, T)], n2 = X[ptix(k + 1, 3, 2, b, T)];
+    const double u0 = U[ptix(k, 2, 0, b, T)], u1 = U[ptix(k, 2, 1, b, T)];
+    const double base = x0 + x1 + x2 + u0 + u1;
+#pragma unroll
+    for (int f = 0; f < 24; ++f) J[ptix(k, 24, f, b, T)] = base + f;
+    x0 = n0;
+    x1 = n1;
+    x2 = n2;
+  }
+}
 // per element of `a`: 1 read, ~4.5 writes (9 writes per 2 reads)
 __global__ void mix(const double2* __restrict__ a, double2* __restrict__ o, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -126,6 +148,18 @@ int main() {
     timeit([&] { hipLaunchKernelGGL(sweep_tiled64, dim3(Bs / 256), dim3(256), 0, 0, ob, Bs, S); }, by,
            "sweep store pattern tiled, 64-instance tiles, 8B/lane");
     CK(hipFree(ob));
+    double *X, *U, *J;
+    CK(hipMalloc(&X, (long)Bs * (S + 1) * 3 * 8));
+    CK(hipMalloc(&U, (long)Bs * S * 2 * 8));
+    CK(hipMalloc(&J, (long)Bs * S * 24 * 8));
+    CK(hipMemset(X, 0, (long)Bs * (S + 1) * 3 * 8));
+    CK(hipMemset(U, 0, (long)Bs * S * 2 * 8));
+    const double byc = (double)Bs * ((S + 1) * 3 * 8 + S * 2 * 8 + S * 24 * 8);
+    timeit([&] { hipLaunchKernelGGL(sweep_copy, dim3(Bs / 256), dim3(256), 0, 0, X, U, J, Bs, S); }, byc,
+           "sweep traffic without arithmetic (compulsory bytes)");
+    CK(hipFree(X));
+    CK(hipFree(U));
+    CK(hipFree(J));
   }
   const long nm = nw / 4;
   timeit([&] { hipLaunchKernelGGL(mix, dim3(grid), dim3(block), 0, 0, a, o, nm); }, nm * 16.0 * (1 + 4.5),
