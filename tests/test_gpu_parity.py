@@ -685,3 +685,27 @@ def test_mpctools_variant_closed_loop_3exemplo(mpcx, R, golden):
     assert us.shape[0] == rows.shape[0]
     assert rel_err(us, rows[:, 3:5]) <= REL_TOL
     assert np.abs(xs - rows[:, 0:3]).max() <= 1e-4
+
+
+def test_iteration_counts_match_cpp_oracle(mpcx, R, C):
+    """Algorithm fidelity, not only the optimum: the kernel and the independently written C++
+    IPOPT restatement take the same number of iterations on the config-2 batch, cold and
+    after one warm-started closed-loop step (IPOPT warm_start_init_point)."""
+    import bench
+    from mpcx import dist
+
+    B, N = 1024, 20
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=N))
+    P = dist.config2_inputs(0, B)
+    r = solver.solve_batch(P)
+    rocp = R.UnicycleOCP(N=N)
+    ref = C.solve_batch(rocp, P, w0=bench._cold(P, N, R), nthreads=0)
+    assert np.mean(r["iters"] == ref["iters"]) >= 0.99
+    # one closed-loop step later, warm-started from the shifted primal-dual solution
+    P2 = P.copy()
+    P2[:, 0:3], _ = R.F(P[:, 0:3], r["w"][:, 3:5], P[:, 3:6], rocp)
+    w0, l0, lx0 = bench.shift_np(r["w"], N), bench.shift_lam_np(r["lam_g"], N), bench.shift_lamx_np(r["lam_x"], N)
+    r2 = solver.solve_batch(P2, w0=w0, lam_g0=l0, lam_x0=lx0)
+    ref2 = C.solve_batch_warm(rocp, P2, w0, lam0=l0, lamx0=lx0, mu_init=1e-4, bound_push=1e-4, mult_push=1e-4,
+                              nthreads=0)
+    assert np.mean(r2["iters"] == ref2["iters"]) >= 0.99
