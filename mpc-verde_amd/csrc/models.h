@@ -21,6 +21,9 @@ struct UnicycleModel {
   static constexpr int NX = 3, NU = 2;
   static constexpr unsigned long long AMASK = (1ull << 0) | (1ull << 2) | (1ull << 4) | (1ull << 5) | (1ull << 8);
   static constexpr unsigned long long BMASK = (1ull << 0) | (1ull << 1) | (1ull << 2) | (1ull << 3) | (1ull << 5);
+  // the line search's first trial evaluates derivatives, not just values: accepted (the
+  // usual case) it is the next iteration's evaluation, which is then skipped
+  static constexpr bool kEvalInSearch = true;
   struct Ctx {
     double xr[3], ur[2];
   };
@@ -57,6 +60,7 @@ struct LinearModel {
   static constexpr int NX = NX_, NU = NU_, NZ = NX_ + NU_, NH = NZ * (NZ + 1) / 2;
   static constexpr unsigned long long AMASK = (NX * NX >= 64) ? ~0ull : ((1ull << (NX * NX)) - 1);
   static constexpr unsigned long long BMASK = (1ull << (NX * NU)) - 1;
+  static constexpr bool kEvalInSearch = false;  // a value is one mat-vec: nothing to save
   struct Ctx {
     const double *A, *B, *c, *W;
     double zr[NZ];

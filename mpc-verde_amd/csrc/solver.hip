@@ -215,12 +215,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   double xf[NX], qv, A[NX * NX], Bm[NX * NU], gq[NZ], Hs[NH];
   double cdef[NX], c0[NX];  // cdef = F(X_k,U_k) - X_{k+1} (constraint k+1), c0 = x0 - X_0 (lane 0)
   double fs = 1.0;
-  auto sweep = [&]() __attribute__((always_inline)) {
+  // evaluation at the point (zz, ll): also the line search's first trial when the model's
+  // kEvalInSearch is set
+  auto eval_at = [&](const double* zz, const double* ll) __attribute__((always_inline)) {
     double ln[NX], xn[NX], own[2 * NX], nxt[2 * NX];
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
-      own[i] = lam[i];
-      own[NX + i] = z[i];
+      own[i] = ll[i];
+      own[NX + i] = zz[i];
     }
     group_next<G, 2 * NX>(own, nxt, xw);
 #pragma unroll
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       ln[i] = nxt[i];
       xn[i] = nxt[NX + i];
     }
-    Model::derivs(ma, ctx, z, ln, fs, xf, qv, A, Bm, gq, Hs);
+    Model::derivs(ma, ctx, zz, ln, fs, xf, qv, A, Bm, gq, Hs);
     const double m = hasU ? 1.0 : 0.0;
     qv *= m;
 #pragma unroll
@@ -238,8 +240,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
       cdef[i] = hasU ? xf[i] - xn[i] : 0.0;
-      c0[i] = (valid && k == 0) ? x0[i] - z[i] : 0.0;
+      c0[i] = (valid && k == 0) ? x0[i] - zz[i] : 0.0;
     }
+  };
+  // fresh: xf .. c0 hold the evaluation at the current (z, lam) (group-uniform)
+  bool fresh = false;
+  auto sweep = [&]() __attribute__((always_inline)) {
+    eval_at(z, lam);
+    fresh = true;
   };
 
   double mu = warm ? a.mu_init : 0.1, tau = fmax(kTauMin, 1.0 - mu);
@@ -322,6 +330,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         lx0[NX + i] = (warm && hasU) ? (lastU ? own[NZ + 2 * NX + i] : nxt[NZ + 2 * NX + i]) : 0.0;
       }
       init_point();
+      fresh = false;
       mu = warm ? a.mu_init : 0.1;
       tau = fmax(kTauMin, 1.0 - mu);
       fs = 1.0;
@@ -341,8 +350,12 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   const long max_pass = (long)K * (a.max_iter + 2);
   for (long pass = 0; pass <= max_pass; ++pass, ++it) {
     if (K > 1) step_boundary();
-    // ------------------------------------------------------------ evaluation (the only call site)
-    sweep();
+    // ------------------------------------------------------------ evaluation
+    //  skipped when the line search already evaluated the accepted point; only the groups
+    //  that need it evaluate (exec-masked, group-uniform), so an instance's sequence of
+    //  evaluation sites -- and its bits -- never depends on its wave neighbours
+    if (__any(!fresh && !done))
+      if (!fresh) sweep();
     if (it == 0) {
       // objective scaling (IPOPT nlp_scaling_method = gradient-based, max_gradient = 100).
       // With lambda scaled by the same factor the Lagrangian's gradient and Hessian scale
@@ -763,6 +776,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     bool searching = !done && !tinystep;
     bool accepted = !done && tinystep;
     bool ftype = tinystep;
+    bool trial_fresh = false;  // accepted at the first trial, which evaluated derivatives
     // switching condition alpha (-gd)^s_phi > delta theta^s_theta  <=>  alpha > sw_a with
     // sw_a = delta theta^s_theta / (-gd)^s_phi -- also the third term of alpha_min; one exp of
     // logs, loop-invariant over the trials
@@ -773,11 +787,22 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       if (!__any(searching)) break;
       double zt[NZ];
 #pragma unroll
-      for (int i = 0; i < NZ; ++i) zt[i] = z[i] + alpha * dz[i];
-      double xtn[NX];
-      group_next<G, NX>(zt, xtn, xw);
+      for (int i = 0; i < NZ; ++i) zt[i] = fma(alpha, dz[i], z[i]);  // the update's exact expression
       double tht_l = 0, pht_l = 0;
-      {
+      if (Model::kEvalInSearch && ls == 0) {
+        if (searching) {  // group-uniform (block-uniform for multi-wave groups)
+          double lt[NX];
+#pragma unroll
+          for (int i = 0; i < NX; ++i) lt[i] = fma(alpha, dlam[i], lam[i]);
+          eval_at(zt, lt);
+          fresh = false;  // until accepted
+#pragma unroll
+          for (int i = 0; i < NX; ++i) tht_l += fabs(cdef[i]) + fabs(c0[i]);
+          pht_l = fs * qv;  // masked to 0 without an interval
+        }
+      } else {
+        double xtn[NX];
+        group_next<G, NX>(zt, xtn, xw);
         double xft[NX], qt;
         Model::value(ma, ctx, zt, xft, qt);
         if (hasU) {
@@ -785,10 +810,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           for (int i = 0; i < NX; ++i) tht_l += fabs(xft[i] - xtn[i]);
           pht_l = fs * qt;
         }
-      }
-      if (valid && k == 0)
+        if (valid && k == 0)
 #pragma unroll
-        for (int i = 0; i < NX; ++i) tht_l += fabs(x0[i] - zt[i]);
+          for (int i = 0; i < NX; ++i) tht_l += fabs(x0[i] - zt[i]);
+      }
       pht_l -= mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU);
       const double tht = gsum<G>(tht_l, xw), pht = gsum<G>(pht_l, xw);
       const double inF = (k < nfilt && tht >= fth && pht >= fph) ? 1.0 : 0.0;
@@ -810,6 +835,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           searching = false;
           accepted = true;
           ftype = ft;
+          trial_fresh = Model::kEvalInSearch && ls == 0;
           if (ft) DIAG(7);
         } else {
           DIAG(2);
@@ -836,9 +862,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         nfilt = nfilt < G ? nfilt + 1 : G;
       }
 #pragma unroll
-      for (int i = 0; i < NZ; ++i) z[i] += alpha * dz[i];
+      for (int i = 0; i < NZ; ++i) z[i] = fma(alpha, dz[i], z[i]);
 #pragma unroll
-      for (int i = 0; i < NX; ++i) lam[i] += alpha * dlam[i];
+      for (int i = 0; i < NX; ++i) lam[i] = fma(alpha, dlam[i], lam[i]);
+      fresh = trial_fresh;
 #pragma unroll
       for (int i = 0; i < NZ; ++i) {
         if (hL[i]) {
@@ -863,7 +890,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   }
 #endif
 
-  // ---- results
+  // ---- results (an instance that ended in a failed line search holds a trial's evaluation)
+  if (__any(!fresh))
+    if (!fresh) sweep();
   const double fsum = gsum<G>(hasU ? qv : 0.0, xw);
 #ifdef MPCX_DEBUG_PRINT
   if (inst == 0 && (k % 64) == 0)
