@@ -354,8 +354,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     //  skipped when the line search already evaluated the accepted point; only the groups
     //  that need it evaluate (exec-masked, group-uniform), so an instance's sequence of
     //  evaluation sites -- and its bits -- never depends on its wave neighbours
-    if (__any(!fresh && !done))
-      if (!fresh) sweep();
+    //  (models without kEvalInSearch evaluate unconditionally: nothing then stays live
+    //  across the back-edge)
+    if constexpr (Model::kEvalInSearch) {
+      if (__any(!fresh && !done))
+        if (!fresh) sweep();
+    } else {
+      sweep();
+    }
     if (it == 0) {
       // objective scaling (IPOPT nlp_scaling_method = gradient-based, max_gradient = 100).
       // With lambda scaled by the same factor the Lagrangian's gradient and Hessian scale
@@ -891,8 +897,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #endif
 
   // ---- results (an instance that ended in a failed line search holds a trial's evaluation)
-  if (__any(!fresh))
-    if (!fresh) sweep();
+  if constexpr (Model::kEvalInSearch) {
+    if (__any(!fresh))
+      if (!fresh) sweep();
+  }
   const double fsum = gsum<G>(hasU ? qv : 0.0, xw);
 #ifdef MPCX_DEBUG_PRINT
   if (inst == 0 && (k % 64) == 0)
