@@ -46,6 +46,28 @@ DATA = {
     5: "synthetic: x0 ~ U([-1,1]x[-.5,.5]x[-.2,.2]x[-.5,.5]), u_prev = 0",
 }
 DYN = {2: "unicycle", 3: "unicycle", 4: "linear LTV lateral (nx=4, nu=1)", 5: "linear LTI cart-pole (nx=5, nu=1)"}
+# BASELINE-named nonlinear variants (--model; mpcx/ode.py, parity unpinned: CPU oracle only)
+VARIANTS = {3: "kin_bicycle", 4: "dyn_bicycle", 5: "cartpole"}
+DATA_V = {
+    "kin_bicycle": "synthetic: config-3 circle (phase ~ U[0,20pi), x0 = ref + N(0,0.1^2)), bicycle inputs v=0.1, "
+                   "delta=atan(L)",
+    "dyn_bicycle": "lane_change.csv path with x and speed x10 (4-8 m/s), start offsets ~ U{0..449}, x0 = ref + noise",
+    "cartpole": "synthetic: hanging start x0 = (U[-1,1], U[-.5,.5], pi+U[-.2,.2], U[-.5,.5]), set point 0",
+}
+DYN_V = {"kin_bicycle": "nonlinear kinematic bicycle (nx=3, nu=2), exact 2nd-order forward-mode derivatives",
+         "dyn_bicycle": "nonlinear 6-state dynamic bicycle, linear tyres (nx=6, nu=2), exact derivatives",
+         "cartpole": "nonlinear cart-pole (nx=4, nu=1), exact derivatives"}
+
+
+def workload_name_v(variant, N, M):
+    return {
+        "kin_bicycle": f"config 3 variant: closed-loop circular tracking, kinematic bicycle, multiple shooting N={N}, "
+                       f"RK4 M={M} node cost, tol 1e-8",
+        "dyn_bicycle": f"config 4 variant: closed-loop lane change, 6-state dynamic bicycle, multiple shooting N={N}, "
+                       f"RK4 M={M} node cost, vx >= 2.5, tol 1e-8",
+        "cartpole": f"config 5 variant: closed-loop cart-pole swing-up, multiple shooting N={N}, RK4 M={M} node cost, "
+                    f"|F| <= 200, tol 1e-8",
+    }[variant]
 
 
 def workload_name(cfg, N):
@@ -69,6 +91,9 @@ def parse():
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5),
                     help="2: point-to-point N=20 B=1024 (headline); 3: circular tracking N=30 B=4096; "
                          "4: LTV lateral lane change N=50 B=1024/GPU; 5: cart-pole QP N=100 B=2048/GPU")
+    ap.add_argument("--model", choices=("default",) + tuple(VARIANTS.values()), default="default",
+                    help="BASELINE-named nonlinear variant of configs 3/4/5: kin_bicycle (3), dyn_bicycle (4), "
+                         "cartpole swing-up (5)")
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU (default per config)")
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--seed", type=int, default=20261015)
@@ -238,6 +263,10 @@ def main():
     from mpcx.device import DeviceLoop
 
     cfg = args.config
+    variant = None if args.model == "default" else args.model
+    if variant is not None and VARIANTS.get(cfg) != variant:
+        raise SystemExit(f"--model {variant} is the variant of config "
+                         f"{[c for c, v in VARIANTS.items() if v == variant][0]}")
     dev = f"cuda:{local}"
     N = args.N or {2: 20, 3: 30, 4: 50, 5: 100}[cfg]
     B = args.batch or {2: 1024, 3: 4096, 4: 1024, 5: 2048}[cfg]
@@ -245,7 +274,10 @@ def main():
     T_all = args.warmup + 2 * args.steps  # warmup, timed multi-step run, lock-step latency run
     per_step = None  # per-step device updates (stage references / schedules), resident in HBM
     seq = lambda t0, K: (None, None)  # noqa: E731  same, as sequences for a multi-step launch
-    if cfg in (2, 3):
+    if variant is not None:
+        ocp = {"kin_bicycle": mpcx.kinematic_bicycle_tracking, "dyn_bicycle": mpcx.dynamic_bicycle_lane_change,
+               "cartpole": mpcx.cartpole_swingup}[variant](N=N)
+    elif cfg in (2, 3):
         ocp = mpcx.unicycle_point_to_point(N=N) if cfg == 2 else mpcx.unicycle_tracking(N=N)
     elif cfg == 4:
         t0, x0, par = mdist.config4_inputs(start, stop, N=N)
@@ -262,7 +294,22 @@ def main():
             print(json.dumps({"sweep_ms": ms, "B": args.roofline_batch, "N": N}))
         return
 
-    if cfg == 2:
+    if variant == "kin_bicycle":  # per-step references on the config-3 circle
+        tau0, P0 = mdist.config3_bicycle_inputs(start, stop, N=N)
+        refs = torch.from_numpy(np.stack([mpcx.ode.bicycle_circular_reference(tau0, t, N).reshape(B, -1)
+                                          for t in range(T_all)])).to(dev)
+        per_step = lambda lp, t: lp.set_stage_refs(refs[t])  # noqa: E731
+        seq = lambda t0, K: (_pseq(refs[t0:t0 + K], P0.shape[1], 3), None)  # noqa: E731
+    elif variant == "dyn_bicycle":  # instance time t0 + t on the scaled lane change
+        t0, x0, (Xp, Yp, Vp) = mdist.config4_bicycle_inputs(start, stop)
+        refs = torch.from_numpy(np.stack([np.stack([mpcx.ode.dyn_bicycle_references(Xp, Yp, Vp, int(ti) + t, N)
+                                                    .reshape(-1) for ti in t0]) for t in range(T_all)])).to(dev)
+        P0 = ocp.params(x0, refs[0].cpu().numpy())
+        per_step = lambda lp, t: lp.set_stage_refs(refs[t])  # noqa: E731
+        seq = lambda t0, K: (_pseq(refs[t0:t0 + K], P0.shape[1], 6), None)  # noqa: E731
+    elif variant == "cartpole":
+        P0 = mdist.config5_swingup_inputs(start, stop)
+    elif cfg == 2:
         P0 = mdist.config2_inputs(start, stop, args.seed)
     elif cfg == 3:  # per-step circular references (Trajectory_tracking.py:84-97)
         tau0, P0 = mdist.config3_inputs(start, stop, N=N)
@@ -338,7 +385,9 @@ def main():
 
     # closed-loop statistics: the only collective (RCCL all_gather over xGMI), outside the timed region
     P_fin = loop.P.cpu().numpy()
-    if cfg == 3:  # final error against the stage-0 reference
+    if variant is not None:  # first three states against the stage-0 reference / set point
+        P_fin = np.concatenate([P_fin[:, 0:3], P_fin[:, ocp.nx:ocp.nx + 3]], axis=1)
+    elif cfg == 3:  # final error against the stage-0 reference
         P_fin = np.concatenate([P_fin[:, 0:3], P_fin[:, 3:6]], axis=1)
     elif cfg == 4:  # (y, phi, v_y) against the stage-0 reference
         P_fin = np.concatenate([P_fin[:, 0:3], P_fin[:, 4:7]], axis=1)
@@ -403,8 +452,9 @@ def main():
                          "iters_max_per_step_mean": round(float(lock_iters_max), 2)},
             "ms_per_solve_p50": round(p50, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64",
-            "data": DATA[cfg],
-            "config": {"workload": workload_name(cfg, N), "dynamics": DYN[cfg], "N": N,
+            "data": DATA_V[variant] if variant else DATA[cfg],
+            "config": {"workload": workload_name_v(variant, N, ocp.M) if variant else workload_name(cfg, N),
+                       "dynamics": DYN_V[variant] if variant else DYN[cfg], "N": N,
                        "M": getattr(ocp, "M", None), "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"instance-sharded x{world} (no data-path collective)"},
             "iters_mean": round(float(S_all[:, 1].mean()), 2), "iters_max": int(S_all[:, 2].max()),

@@ -46,7 +46,15 @@ enum mpcx_model {
      LTI/LTV QPs (Inverted_pendulum/inverted_pendulum_single_shooting_mpctools.py:19-64,
      Trajectory Tracking/Trajectory_tracking_dynamic_model.py:117-145); tables set with
      mpcx_set_linear_model.  (nx, nu) in {(4,1), (5,1)}. */
-  MPCX_MODEL_LINEAR = 2
+  MPCX_MODEL_LINEAR = 2,
+  /* Nonlinear ODE models (BASELINE config variants; parity against the CPU oracle only),
+     RK4 with M substeps, node cost l = sum Q_i (x_i - xr_i)^2 + sum R_j (u_j - ur_j)^2,
+     exact derivatives (mpc-verde_amd/csrc/ode.h).  Constants in mpcx_spec.par. */
+  MPCX_MODEL_KIN_BICYCLE = 3, /* x=(X,Y,psi), u=(v,delta); par = (L) */
+  MPCX_MODEL_DYN_BICYCLE = 4, /* x=(X,Y,psi,vx,vy,r), u=(delta,ax), linear tyres; par = (m,a,b,Ca,Jz):
+                                 the nonlinear parent of Trajectory_tracking_dynamic_model.py:119-128 */
+  MPCX_MODEL_CARTPOLE = 5     /* x=(p,p',phi,phi'), u=F; par = (M,m,L,g,c): the nonlinear parent of
+                                 inverted_pendulum_single_shooting_mpctools.py:19-23 */
 };
 
 enum mpcx_cost {
@@ -100,11 +108,14 @@ typedef struct mpcx_spec {
      push and bound-multiplier push.  Defaults 1e-4. */
   double warm_mu_init, warm_bound_push, warm_mult_push;
   int32_t nx, nu;       /* state / control dimensions (unicycle: 3, 2) */
+  double par[8];        /* model constants of the ODE models (see mpcx_model) */
 } mpcx_spec;
 
 /* Fill *s with the reference's constants for model/cost at horizon N
    (unicycle point-to-point: T=0.2, M=4, Q=diag(1,5,0.1), R=diag(0.5,0.05),
-   |v|<=1, |omega|<=pi/4, max_iter=2000, tol=1e-8). */
+   |v|<=1, |omega|<=pi/4, max_iter=2000, tol=1e-8).  ODE models: node cost, M=1,
+   param_layout MPCX_P_X0_STAGEREF (cart-pole: MPCX_P_X0_XREF), the constants listed
+   at mpcx_model and the defaults of mpcx/ode.py. */
 int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N);
 
 int mpcx_create(const mpcx_spec* s, mpcx_handle** h);

@@ -56,8 +56,35 @@ int hipfail(hipError_t e, const char* where) {
     if (e_ != hipSuccess) return hipfail(e_, #expr);   \
   } while (0)
 
-int nx_of(const mpcx_spec& s) { return s.model == MPCX_MODEL_UNICYCLE ? 3 : s.nx; }
-int nu_of(const mpcx_spec& s) { return s.model == MPCX_MODEL_UNICYCLE ? 2 : s.nu; }
+// (nx, nu) fixed by the model; the linear model takes them from the spec
+int nx_of(const mpcx_spec& s) {
+  switch (s.model) {
+    case MPCX_MODEL_UNICYCLE: case MPCX_MODEL_KIN_BICYCLE: return 3;
+    case MPCX_MODEL_DYN_BICYCLE: return 6;
+    case MPCX_MODEL_CARTPOLE: return 4;
+    default: return s.nx;
+  }
+}
+int nu_of(const mpcx_spec& s) {
+  switch (s.model) {
+    case MPCX_MODEL_UNICYCLE: case MPCX_MODEL_KIN_BICYCLE: case MPCX_MODEL_DYN_BICYCLE: return 2;
+    case MPCX_MODEL_CARTPOLE: return 1;
+    default: return s.nu;
+  }
+}
+bool is_ode(int model) { return model >= MPCX_MODEL_KIN_BICYCLE && model <= MPCX_MODEL_CARTPOLE; }
+
+mpcx::OdeParams ode_params(const mpcx_spec& s) {
+  mpcx::OdeParams op{};
+  op.M = s.M;
+  op.h = s.T / s.M;
+  for (int i = 0; i < 8; ++i) {
+    op.Q[i] = s.Q[i];
+    op.R[i] = s.R[i];
+    op.par[i] = s.par[i];
+  }
+  return op;
+}
 
 mpcx::StageParams stage_params(const mpcx_spec& s) {
   mpcx::StageParams sp;
@@ -167,7 +194,7 @@ const char* mpcx_last_error(void) { return g_err.c_str(); }
 
 int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N) {
   if (!s) return fail(MPCX_EINVAL, "null spec");
-  if (model != MPCX_MODEL_UNICYCLE) return fail(MPCX_EINVAL, "unknown model");
+  if (model != MPCX_MODEL_UNICYCLE && !is_ode(model)) return fail(MPCX_EINVAL, "unknown model");
   std::memset(s, 0, sizeof *s);
   // Casadi/multiple_shooting_casadi.py:30-45, 78-84, 101, 188-196
   s->model = model;
@@ -192,17 +219,56 @@ int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N) {
   s->warm_mu_init = 1e-4;
   s->warm_bound_push = 1e-4;
   s->warm_mult_push = 1e-4;
+  if (is_ode(model)) {  // defaults of the BASELINE config variants (mpcx/ode.py documents them)
+    s->cost = MPCX_COST_NODE;
+    s->param_layout = MPCX_P_X0_STAGEREF;
+    s->M = 1;
+    s->nx = nx_of(*s);
+    s->nu = nu_of(*s);
+    for (int i = 0; i < 8; ++i) {
+      s->Q[i] = s->R[i] = 0.0;
+      s->lbx[i] = -1e20;
+      s->ubx[i] = 1e20;
+    }
+  }
+  if (model == MPCX_MODEL_KIN_BICYCLE) {  // config 3 variant: circular tracking, T = 0.2
+    s->Q[0] = 1.0; s->Q[1] = 1.0; s->Q[2] = 0.1;
+    s->R[0] = 0.5; s->R[1] = 0.05;
+    s->lbu[0] = -1.0; s->ubu[0] = 1.0;
+    s->lbu[1] = -M_PI / 4; s->ubu[1] = M_PI / 4;
+    s->par[0] = 0.5;  // wheelbase L
+  } else if (model == MPCX_MODEL_DYN_BICYCLE) {  // config 4 variant: lane change, T = 0.05
+    s->T = 0.05;
+    s->M = 4;  // RK4 stability at 4-8 m/s (|A44| h <= 1.6)
+    for (int i = 0; i < 6; ++i) s->Q[i] = 1.0;  // Trajectory_tracking_dynamic_model.py:23-31 (Q = I, R = 1)
+    s->R[0] = 1.0; s->R[1] = 1.0;
+    s->lbu[0] = -0.5; s->ubu[0] = 0.5;  // steering [rad]
+    s->lbu[1] = -5.0; s->ubu[1] = 5.0;  // longitudinal acceleration [m/s^2]
+    s->lbx[3] = 2.5;                    // vx >= 2.5 m/s: RK4 (M = 4) stays stable, |A44| h <= 2.55
+    const double par[5] = {1200.0, 1.5, 2.0, 55000.0, 1350.0};  // :36-40
+    for (int i = 0; i < 5; ++i) s->par[i] = par[i];
+  } else if (model == MPCX_MODEL_CARTPOLE) {  // config 5 variant: swing-up, T = 0.01
+    s->T = 0.01;
+    s->param_layout = MPCX_P_X0_XREF;
+    s->Q[0] = 1.44; s->Q[2] = 1.0;  // l = (1.2 (p - p_ref))^2 + phi^2 (inverted_pendulum...py:33-36)
+    s->R[0] = 1e-4;                 // (0.01 u)^2
+    s->lbu[0] = -200.0; s->ubu[0] = 200.0;  // :28
+    const double par[5] = {1.0, 1.0, 0.5, 9.81, 10.0};
+    for (int i = 0; i < 5; ++i) s->par[i] = par[i];
+  }
   return 0;
 }
 
 int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
   if (!s || !out) return fail(MPCX_EINVAL, "null argument");
-  if (s->model != MPCX_MODEL_UNICYCLE && s->model != MPCX_MODEL_LINEAR) return fail(MPCX_EINVAL, "unknown model");
+  if (s->model != MPCX_MODEL_UNICYCLE && s->model != MPCX_MODEL_LINEAR && !is_ode(s->model))
+    return fail(MPCX_EINVAL, "unknown model");
+  if (is_ode(s->model) && s->cost != MPCX_COST_NODE) return fail(MPCX_EINVAL, "ODE models use MPCX_COST_NODE");
   if (s->model == MPCX_MODEL_LINEAR && !((s->nx == 4 && s->nu == 1) || (s->nx == 5 && s->nu == 1)))
     return fail(MPCX_EINVAL, "linear model: (nx, nu) must be (4, 1) or (5, 1)");
   if (s->N < 1 || s->N > 255) return fail(MPCX_EINVAL, "N must be in [1, 255]");
   if (s->M < 1 || s->M > 64) return fail(MPCX_EINVAL, "M must be in [1, 64]");
-  if (s->model == MPCX_MODEL_UNICYCLE && !(s->T > 0)) return fail(MPCX_EINVAL, "T must be > 0");
+  if ((s->model == MPCX_MODEL_UNICYCLE || is_ode(s->model)) && !(s->T > 0)) return fail(MPCX_EINVAL, "T must be > 0");
   if (s->cost != MPCX_COST_QUADRATURE && s->cost != MPCX_COST_NODE) return fail(MPCX_EINVAL, "unknown cost");
   if (s->param_layout != MPCX_P_X0_XREF && s->param_layout != MPCX_P_X0_STAGEREF)
     return fail(MPCX_EINVAL, "unknown param_layout");
@@ -346,6 +412,7 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
   a.p_stride = h->np;
   a.tol = h->spec.tol;
   a.sp = stage_params(h->spec);
+  a.op = ode_params(h->spec);
   a.P = P;
   a.w0 = w0;
   a.lam0 = lam0;

@@ -60,7 +60,7 @@ struct OpMin {
 // exchange can never overwrite values a slower wave is still reading (a wave can be at
 // most one barrier ahead).  All waves execute the same sequence of exchanges because
 // every branch around them is group-uniform.
-constexpr int kXchStride = 32;  // doubles per wave per slot (>= NP + NX and NX^2 + NX of the largest model)
+constexpr int kXchStride = 48;  // doubles per wave per slot (>= NP + NX and NX^2 + NX of the largest model)
 template <int G>
 struct XWave {
   static constexpr int W = G > 64 ? G / 64 : 1;

@@ -1,0 +1,252 @@
+// ode.h -- nonlinear ODE stage models with exact derivatives by second-order forward mode.
+//
+// The BASELINE configs name three nonlinear models that the reference only has in linearised
+// or renamed form.  Each is written once, templated on its scalar
+// type, and integrated by the same RK4 as the unicycle (M substeps of h = T/M):
+//
+//   KinBicycle   x = (X, Y, psi), u = (v, delta); psi' = v tan(delta) / L
+//                (the "kinematic bicycle" of config 3; Trajectory Tracking/Trajectory_tracking.py
+//                tracks with a unicycle)
+//   DynBicycle   x = (X, Y, psi, vx, vy, r), u = (delta, ax), linear tyres with the
+//                reference's constants m, a, b, Ca, Jz (Trajectory_tracking_dynamic_model.py:36-42).
+//                Its linearisation at vx = vref, small delta, is exactly the reference's LTV
+//                lateral model (:119-128, A34 with the intended precedence).
+//   CartPole     x = (p, p', phi, phi'), u = F; M, m, L, g, friction c.  Its linearisation at
+//                phi = 0 is exactly the reference's Ac, Bc with M = m = 1, L = 0.5, c = 10
+//                (Inverted_pendulum/inverted_pendulum_single_shooting_mpctools.py:19-23).
+//
+// Derivatives.  A hyper-dual number v + a e1 + b e2 + ab e1e2 (e1^2 = e2^2 = 0) carries the
+// first derivatives along two seed directions and the mixed second derivative.  One RK4 pass
+// seeded with (e_i, e_j) gives columns i and j of dF/dz and d2F/dz_i dz_j exactly (no
+// truncation).  Passes run over the pairs of variables that enter f nonlinearly (NLMASK) plus
+// one pass per remaining variable; the passes share one RK4 body (runtime loop) so code size
+// does not grow with the pair count.  The stage cost is the mpctools node cost
+// l = sum Q_i (x_i - xr_i)^2 + sum R_j (u_j - ur_j)^2 (exact gradient and Hessian in closed form).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "riccati.h"
+#include "solver.h"
+
+namespace mpcx {
+
+using ::cos;  // the double overloads stay visible next to the HD ones below
+using ::sin;
+using ::tan;
+
+struct HD {
+  double v, a, b, ab;
+};
+__device__ __forceinline__ HD operator+(HD x, HD y) { return {x.v + y.v, x.a + y.a, x.b + y.b, x.ab + y.ab}; }
+__device__ __forceinline__ HD operator-(HD x, HD y) { return {x.v - y.v, x.a - y.a, x.b - y.b, x.ab - y.ab}; }
+__device__ __forceinline__ HD operator-(HD x) { return {-x.v, -x.a, -x.b, -x.ab}; }
+__device__ __forceinline__ HD operator+(HD x, double c) { return {x.v + c, x.a, x.b, x.ab}; }
+__device__ __forceinline__ HD operator+(double c, HD x) { return {x.v + c, x.a, x.b, x.ab}; }
+__device__ __forceinline__ HD operator-(HD x, double c) { return {x.v - c, x.a, x.b, x.ab}; }
+__device__ __forceinline__ HD operator-(double c, HD x) { return {c - x.v, -x.a, -x.b, -x.ab}; }
+__device__ __forceinline__ HD operator*(HD x, double c) { return {x.v * c, x.a * c, x.b * c, x.ab * c}; }
+__device__ __forceinline__ HD operator*(double c, HD x) { return {x.v * c, x.a * c, x.b * c, x.ab * c}; }
+__device__ __forceinline__ HD operator*(HD x, HD y) {
+  return {x.v * y.v, fma(x.a, y.v, x.v * y.a), fma(x.b, y.v, x.v * y.b),
+          fma(x.ab, y.v, fma(x.a, y.b, fma(x.b, y.a, x.v * y.ab)))};
+}
+__device__ __forceinline__ HD recip(HD y) {
+  const double r = 1.0 / y.v, m = -r * r;  // d(1/y) = -y'/y^2, d2 = -y''/y^2 + 2 y'_a y'_b / y^3
+  return {r, m * y.a, m * y.b, fma(m, y.ab, -2.0 * m * r * y.a * y.b)};
+}
+__device__ __forceinline__ HD operator/(HD x, HD y) { return x * recip(y); }
+__device__ __forceinline__ HD operator/(double c, HD y) { return c * recip(y); }
+__device__ __forceinline__ HD sin(HD x) {
+  double s, c;
+  sincos(x.v, &s, &c);
+  return {s, c * x.a, c * x.b, fma(c, x.ab, -s * x.a * x.b)};
+}
+__device__ __forceinline__ HD cos(HD x) {
+  double s, c;
+  sincos(x.v, &s, &c);
+  return {c, -s * x.a, -s * x.b, -fma(s, x.ab, c * x.a * x.b)};
+}
+__device__ __forceinline__ HD tan(HD x) {
+  const double t = ::tan(x.v), d = fma(t, t, 1.0);  // tan' = 1 + tan^2, tan'' = 2 tan (1 + tan^2)
+  return {t, d * x.a, d * x.b, fma(d, x.ab, 2.0 * t * d * x.a * x.b)};
+}
+
+// ---------------------------------------------------------------------------- dynamics
+struct KinBicycle {
+  static constexpr int NX = 3, NU = 2;
+  static constexpr unsigned NLMASK = (1u << 2) | (1u << 3) | (1u << 4);  // psi, v, delta
+  static constexpr unsigned INDEP = (1u << 0) | (1u << 1);               // f does not read X, Y
+  template <class S>
+  __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx) {
+    dx[0] = u[0] * cos(x[2]);
+    dx[1] = u[0] * sin(x[2]);
+    dx[2] = u[0] * tan(u[1]) * (1.0 / par[0]);  // par = (L)
+  }
+};
+
+struct DynBicycle {
+  static constexpr int NX = 6, NU = 2;
+  // psi, vx, vy, r, delta (ax enters linearly, X and Y not at all)
+  static constexpr unsigned NLMASK = (1u << 2) | (1u << 3) | (1u << 4) | (1u << 5) | (1u << 6);
+  static constexpr unsigned INDEP = (1u << 0) | (1u << 1);
+  template <class S>
+  __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx) {
+    // par = (m, a, b, Ca, Jz): Trajectory_tracking_dynamic_model.py:36-40 (a, b = CG-axle distances)
+    const double m = par[0], a = par[1], b = par[2], Ca2 = 2.0 * par[3], Jz = par[4];
+    const S psi = x[2], vx = x[3], vy = x[4], r = x[5], d = u[0];
+    const S ivx = 1.0 / vx;
+    const S Fyf = Ca2 * (d - (vy + a * r) * ivx);  // front axle: slip angle delta - (vy + a r)/vx
+    const S Fyr = -Ca2 * ((vy - b * r) * ivx);     // rear axle: -(vy - b r)/vx
+    const S sp = sin(psi), cp = cos(psi), sd = sin(d), cd = cos(d);
+    dx[0] = vx * cp - vy * sp;
+    dx[1] = vx * sp + vy * cp;
+    dx[2] = r;
+    dx[3] = u[1] + r * vy - Fyf * sd * (1.0 / m);
+    dx[4] = (Fyf * cd + Fyr) * (1.0 / m) - vx * r;
+    dx[5] = (a * (Fyf * cd) - b * Fyr) * (1.0 / Jz);
+  }
+};
+
+struct CartPole {
+  static constexpr int NX = 4, NU = 1;
+  static constexpr unsigned NLMASK = (1u << 1) | (1u << 2) | (1u << 3) | (1u << 4);  // p', phi, phi', F
+  static constexpr unsigned INDEP = (1u << 0);                                        // f does not read p
+  template <class S>
+  __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx) {
+    // par = (M, m, L, g, c); phi measured so that the upright linearisation is the reference's Ac
+    const double Mc = par[0], m = par[1], L = par[2], g = par[3], c = par[4];
+    const S s = sin(x[2]), co = cos(x[2]);
+    const S pdd = (u[0] - c * x[1] - (m * L) * (x[3] * x[3]) * s + (m * g) * (s * co)) / (Mc + m * (s * s));
+    dx[0] = x[1];
+    dx[1] = pdd;
+    dx[2] = x[3];
+    dx[3] = (g * s + co * pdd) * (1.0 / L);
+  }
+};
+
+// RK4, M substeps, one f call site (the four stages are a runtime loop)
+template <class Dyn, class S>
+__device__ __forceinline__ void ode_rk4(const S* x0, const S* u, const OdeParams& op, S* xf) {
+  constexpr int NX = Dyn::NX;
+  S x[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) x[i] = x0[i];
+  const double h = op.h;
+#pragma unroll 1
+  for (int s = 0; s < op.M; ++s) {
+    S acc[NX], xt[NX], k[NX];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) xt[i] = x[i];
+#pragma unroll 1
+    for (int st = 0; st < 4; ++st) {
+      Dyn::f(xt, u, op.par, k);
+      const double wa = (st == 0 || st == 3) ? 1.0 : 2.0;  // k1 + 2 k2 + 2 k3 + k4
+      const double cn = (st == 2) ? h : 0.5 * h;           // next stage point x + c k
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        acc[i] = st == 0 ? k[i] : acc[i] + wa * k[i];
+        xt[i] = x[i] + cn * k[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) x[i] = x[i] + (h / 6.0) * acc[i];
+  }
+#pragma unroll
+  for (int i = 0; i < NX; ++i) xf[i] = x[i];
+}
+
+template <class Dyn>
+struct OdeModel {
+  static constexpr int NX = Dyn::NX, NU = Dyn::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2;
+  // a column of A is the unit vector e_j when f does not read x_j (F = x + h/6 (...))
+  static constexpr unsigned long long amask() {
+    unsigned long long m = 0;
+    for (int c = 0; c < NX; ++c)
+      for (int j = 0; j < NX; ++j)
+        if (!((Dyn::INDEP >> j) & 1u) || c == j) m |= 1ull << (c * NX + j);
+    return m;
+  }
+  static constexpr unsigned long long AMASK = amask();
+  static constexpr unsigned long long BMASK = (1ull << (NX * NU)) - 1;
+  static constexpr bool kEvalInSearch = false;
+  struct Ctx {
+    double zr[NZ];
+  };
+  __device__ __forceinline__ static void load_ctx(const ModelArgs& a, int inst, const double* P, int k, bool hasU, Ctx& c) {
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) c.zr[i] = 0.0;
+    if (a.p_layout == 0) {
+#pragma unroll
+      for (int i = 0; i < NX; ++i) c.zr[i] = P[NX + i];
+    } else if (hasU) {
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) c.zr[i] = P[NX + NZ * k + i];
+    }
+  }
+  __device__ __forceinline__ static double wgt(const ModelArgs& a, int i) { return i < NX ? a.op.Q[i] : a.op.R[i - NX]; }
+  __device__ __forceinline__ static void value(const ModelArgs& a, const Ctx& c, const double* z, double* xf, double& q) {
+    ode_rk4<Dyn, double>(z, z + NX, a.op, xf);
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+      const double d = z[i] - c.zr[i];
+      acc = fma(wgt(a, i) * d, d, acc);
+    }
+    q = acc;
+  }
+  __device__ __forceinline__ static void derivs(const ModelArgs& a, const Ctx& c, const double* z, const double* ln, double fs,
+                                                double* xf, double& q, double* A, double* Bm, double* g, double* H) {
+    value(a, c, z, xf, q);
+#pragma unroll
+    for (int i = 0; i < NH; ++i) H[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+      const double w2 = 2.0 * fs * wgt(a, i);
+      g[i] = w2 * (z[i] - c.zr[i]);
+      H[symix(i, i, NZ)] = w2;
+    }
+#pragma unroll
+    for (int i = 0; i < NX * NX; ++i) A[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NX * NU; ++i) Bm[i] = 0.0;
+    // passes (m, n): every pair of nonlinear variables, and (m, m) for the others
+#pragma unroll 1
+    for (int m = 0; m < NZ; ++m) {
+      const bool nlm = (Dyn::NLMASK >> m) & 1u;
+#pragma unroll 1
+      for (int n = m; n < NZ; ++n) {
+        if (n != m && !(nlm && ((Dyn::NLMASK >> n) & 1u))) continue;
+        if (m < NX && n == m && ((Dyn::INDEP >> m) & 1u)) {  // column e_m, no curvature
+#pragma unroll
+          for (int r = 0; r < NX; ++r)
+#pragma unroll
+            for (int j = 0; j < NX; ++j)
+              if (j == m) A[r * NX + j] = r == j ? 1.0 : 0.0;
+          continue;
+        }
+        HD zs[NZ], xs[NX];
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) zs[i] = HD{z[i], i == m ? 1.0 : 0.0, i == n ? 1.0 : 0.0, 0.0};
+        ode_rk4<Dyn, HD>(zs, zs + NX, a.op, xs);
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < NX; ++r) {
+          s = fma(ln[r], xs[r].ab, s);
+#pragma unroll
+          for (int j = 0; j < NZ; ++j) {
+            double* e = j < NX ? &A[r * NX + j] : &Bm[r * NU + (j - NX)];
+            if (j == m) *e = xs[r].a;
+            else if (j == n) *e = xs[r].b;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NZ; ++i)
+#pragma unroll
+          for (int j = i; j < NZ; ++j)
+            if (i == m && j == n) H[symix(i, j, NZ)] += s;
+      }
+    }
+  }
+};
+
+}  // namespace mpcx

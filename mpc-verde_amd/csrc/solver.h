@@ -18,6 +18,13 @@ struct LinTables {
   int n_tab;
 };
 
+// Constants of the nonlinear ODE models (ode.h): RK4 substep, node-cost weights, model constants.
+struct OdeParams {
+  double h;  // T / M
+  int M;
+  double Q[8], R[8], par[8];
+};
+
 struct SolveArgs {
   int B, N, max_iter, p_layout;
   int p_stride;
@@ -25,6 +32,7 @@ struct SolveArgs {
   double tol;
   StageParams sp;       // unicycle constants
   LinTables lin;        // linear model tables
+  OdeParams op;         // nonlinear ODE models
   const double* P;      // B x p_stride (device)
   const double* w0;     // B x nw or null (cold start: X_k = x0, U = 0)
   const double* lam0;   // B x ng initial constraint multipliers or null
@@ -58,9 +66,10 @@ struct SolveArgs {
 struct ModelArgs {
   StageParams sp;
   LinTables lin;
+  OdeParams op;
   int p_layout, N;
 };
-__host__ __device__ inline ModelArgs model_args(const SolveArgs& a) { return ModelArgs{a.sp, a.lin, a.p_layout, a.N}; }
+__host__ __device__ inline ModelArgs model_args(const SolveArgs& a) { return ModelArgs{a.sp, a.lin, a.op, a.p_layout, a.N}; }
 
 hipError_t launch_solve(const SolveArgs& a, hipStream_t stream);
 hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X, const double* U, const double* XR,

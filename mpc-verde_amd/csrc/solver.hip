@@ -24,6 +24,7 @@
 
 #include "collectives.h"
 #include "models.h"
+#include "ode.h"
 #include "riccati.h"
 #include "solver.h"
 
@@ -1139,6 +1140,9 @@ static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
     if ((a).model == 1) return FN<UnicycleModel>(__VA_ARGS__);                                   \
     if ((a).model == 2 && (a).nx == 4 && (a).nu == 1) return FN<LinearModel<4, 1>>(__VA_ARGS__); \
     if ((a).model == 2 && (a).nx == 5 && (a).nu == 1) return FN<LinearModel<5, 1>>(__VA_ARGS__); \
+    if ((a).model == 3) return FN<OdeModel<KinBicycle>>(__VA_ARGS__);                            \
+    if ((a).model == 4) return FN<OdeModel<DynBicycle>>(__VA_ARGS__);                            \
+    if ((a).model == 5) return FN<OdeModel<CartPole>>(__VA_ARGS__);                              \
     return hipErrorInvalidValue;                                                                 \
   } while (0)
 

@@ -15,6 +15,9 @@ LIB_PATH = os.environ.get("MPCX_LIB", os.path.join(_HERE, "libmpcx.so"))
 
 MODEL_UNICYCLE = 1
 MODEL_LINEAR = 2
+MODEL_KIN_BICYCLE = 3
+MODEL_DYN_BICYCLE = 4
+MODEL_CARTPOLE = 5
 COST_QUADRATURE = 0
 COST_NODE = 1
 P_X0_XREF = 0
@@ -41,7 +44,7 @@ class Spec(ctypes.Structure):
                 ("lbu", ctypes.c_double * 8), ("ubu", ctypes.c_double * 8), ("lbx", ctypes.c_double * 8),
                 ("ubx", ctypes.c_double * 8), ("warm_mu_init", ctypes.c_double),
                 ("warm_bound_push", ctypes.c_double), ("warm_mult_push", ctypes.c_double),
-                ("nx", ctypes.c_int32), ("nu", ctypes.c_int32)]
+                ("nx", ctypes.c_int32), ("nu", ctypes.c_int32), ("par", ctypes.c_double * 8)]
 
 
 _lib = None

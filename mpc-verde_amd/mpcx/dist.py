@@ -145,6 +145,51 @@ def config5_inputs(start: int, stop: int, seed: int = 20261018):
     return x0
 
 
+def config3_bicycle_inputs(start: int, stop: int, N: int = 30, seed: int = 20261016, L: float = 0.5):
+    """Config 3 variant (kinematic bicycle on the config-3 circle): tau0 ~ U[0, 20 pi),
+    x0 = ref(tau0) + N(0, 0.1^2 I).  Returns (tau0 (n,), P (n, 3 + 5N))."""
+    from .ode import bicycle_circular_reference
+
+    n = stop - start
+    tau0 = np.zeros(n)
+    x0 = np.zeros((n, 3))
+    for i, g in enumerate(range(start, stop)):
+        rng = np.random.default_rng([seed, g])
+        tau0[i] = rng.uniform(0.0, 20.0 * np.pi)
+        x0[i] = bicycle_circular_reference(tau0[i:i + 1], 0, 1, L=L)[0, 0, 0:3] + rng.normal(scale=0.1, size=3)
+    P = np.concatenate([x0, bicycle_circular_reference(tau0, 0, N, L=L).reshape(n, 5 * N)], axis=1)
+    return tau0, P
+
+
+def config4_bicycle_inputs(start: int, stop: int, seed: int = 20261017):
+    """Config 4 variant (6-state dynamic bicycle on the scaled lane change, mpcx/ode.py): start
+    offset t0 ~ U{0..449}, x0 = ref(t0) + N(0, diag(.2, .2, .05, .3, .1, .05)^2).
+    Returns (t0 (n,) int, x0 (n, 6), (X, Y, V) path rows)."""
+    from .ode import dyn_bicycle_references, lane_change_rows
+
+    X, Y, V = lane_change_rows(*lane_change())
+    n = stop - start
+    t0 = np.zeros(n, np.int64)
+    x0 = np.zeros((n, 6))
+    for i, g in enumerate(range(start, stop)):
+        rng = np.random.default_rng([seed, g])
+        t0[i] = rng.integers(0, 450)
+        x0[i] = dyn_bicycle_references(X, Y, V, int(t0[i]), 1)[0, 0:6] + \
+            rng.normal(scale=[0.2, 0.2, 0.05, 0.3, 0.1, 0.05])
+    return t0, x0, (X, Y, V)
+
+
+def config5_swingup_inputs(start: int, stop: int, seed: int = 20261018):
+    """Config 5 variant (cart-pole swing-up): x0 = (U[-1,1], U[-.5,.5], pi + U[-.2,.2], U[-.5,.5]),
+    set point 0.  Returns P (n, 8) = [x0; x_ref]."""
+    n = stop - start
+    P = np.zeros((n, 8))
+    for i, g in enumerate(range(start, stop)):
+        P[i, 0:4] = np.random.default_rng([seed, g]).uniform([-1, -.5, -.2, -.5], [1, .5, .2, .5])
+        P[i, 2] += np.pi
+    return P
+
+
 def stats_matrix(P, w, f, status, iters_hist):
     """Per-instance closed-loop statistics, (B, len(STAT_FIELDS)) float64."""
     B = P.shape[0]

@@ -29,6 +29,7 @@ import numpy as np
 from . import _lib
 from .lti import LinearOCP
 from .ocp import OCP, to_spec
+from .ode import OdeOCP
 
 
 def _vec(v, n, name, fill=None):
@@ -268,8 +269,8 @@ def nlpsol(name: str, plugin: str, prob: OCP, opts: dict | None = None, device: 
     """Create a solver (``ca.nlpsol`` signature).  plugin must be 'mi355x'."""
     if plugin not in ("mi355x",):
         raise ValueError(f"unknown plugin {plugin!r} (available: 'mi355x')")
-    if not isinstance(prob, (OCP, LinearOCP)):
-        raise TypeError("prob must be an mpcx.OCP or mpcx.LinearOCP (symbolic CasADi problems are not supported)")
+    if not isinstance(prob, (OCP, LinearOCP, OdeOCP)):
+        raise TypeError("prob must be an mpcx.OCP, LinearOCP or OdeOCP (symbolic CasADi problems are not supported)")
     return Solver(name, prob, opts, device)
 
 

@@ -99,14 +99,21 @@ def circular_reference(tau0, t, N, Delta=0.2):
     return np.stack([np.cos(0.1 * tau), np.sin(0.1 * tau), np.pi / 2 + 0.1 * tau, one, one], axis=-1)
 
 
+MODEL_IDS = {"unicycle": _lib.MODEL_UNICYCLE, "linear": _lib.MODEL_LINEAR, "kin_bicycle": _lib.MODEL_KIN_BICYCLE,
+             "dyn_bicycle": _lib.MODEL_DYN_BICYCLE, "cartpole": _lib.MODEL_CARTPOLE}
+
+
 def to_spec(ocp, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4)) -> _lib.Spec:
-    """mpcx_spec of an :class:`OCP` (unicycle) or :class:`mpcx.lti.LinearOCP` (linear model;
-    its stage tables are uploaded separately by the solver, mpcx_set_linear_model)."""
-    if ocp.model not in ("unicycle", "linear"):
+    """mpcx_spec of an :class:`OCP` (unicycle), :class:`mpcx.lti.LinearOCP` (linear model;
+    its stage tables are uploaded separately by the solver, mpcx_set_linear_model) or
+    :class:`mpcx.ode.OdeOCP` (nonlinear ODE models, constants in ``par``)."""
+    if ocp.model not in MODEL_IDS:
         raise ValueError(f"unsupported model {ocp.model!r}")
     s = _lib.Spec()
     lin = ocp.model == "linear"
-    s.model = _lib.MODEL_LINEAR if lin else _lib.MODEL_UNICYCLE
+    s.model = MODEL_IDS[ocp.model]
+    for i, v in enumerate(getattr(ocp, "par", ())):
+        s.par[i] = float(v)
     s.cost = {"quadrature": _lib.COST_QUADRATURE, "node": _lib.COST_NODE}[ocp.cost]
     s.param_layout = {"x0_xref": _lib.P_X0_XREF, "x0_stageref": _lib.P_X0_STAGEREF}[ocp.param]
     s.N, s.M, s.max_iter, s.device = int(ocp.N), int(getattr(ocp, "M", 1)), int(max_iter), int(device)

@@ -1,0 +1,148 @@
+"""GPU parity tests of the nonlinear ODE model variants (kinematic bicycle, 6-state dynamic bicycle,
+cart-pole; mpcx/ode.py) through the C ABI.
+
+PARITY UNPINNED (BASELINE-named extensions, no reference outputs): checked against the CPU oracle
+oracle/ode_ref.py (complex-step derivatives, projected Newton; its linearisations are pinned to the
+reference's matrices in tests/test_ode_cpu.py).  Tolerances: plant 1e-12 relative; optimal inputs
+1e-6 relative to max(|u|_inf, 1) at solver tol 1e-10 (north-star bound 1e-4);
+KKT residual of the GPU's primal-dual point, evaluated by the oracle, <= 1e-6.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+U_TOL = 1e-6
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1.0))
+
+
+@pytest.fixture(scope="module")
+def mpcx():
+    import mpcx as m
+
+    m._lib.load()
+    return m
+
+
+def _lane_change():
+    import pandas as pd
+    from mpcx import ode
+
+    g = pd.read_csv(os.path.join(ROOT, "tests", "golden", "lane_change.csv"))
+    return ode.lane_change_rows(g.x, g.y, g.uref)
+
+
+def cases(which, B, N, seed=0):
+    """(ocp, P (B, n_p)) of a small seeded batch."""
+    from mpcx import ode
+
+    rng = np.random.default_rng(seed)
+    if which == "kin_bicycle":
+        ocp = ode.kinematic_bicycle_tracking(N=N)
+        tau0 = rng.uniform(0, 20 * math.pi, B)
+        ref = ode.bicycle_circular_reference(tau0, 0, N)
+        x0 = ref[:, 0, :3] + rng.normal(0, 0.1, (B, 3))
+        return ocp, ocp.params(x0, ref)
+    if which == "dyn_bicycle":
+        ocp = ode.dynamic_bicycle_lane_change(N=N)
+        X, Y, V = _lane_change()
+        t = rng.integers(0, 440, B)
+        ref = np.stack([ode.dyn_bicycle_references(X, Y, V, int(ti), N) for ti in t])
+        x0 = ref[:, 0, :6] + rng.normal(0, 1, (B, 6)) * np.array([0.2, 0.2, 0.05, 0.3, 0.1, 0.05])
+        return ocp, ocp.params(x0, ref)
+    ocp = ode.cartpole_swingup(N=N)
+    x0 = rng.uniform(-1, 1, (B, 4)) * np.array([0.5, 0.3, 0.3, 0.3])
+    xr = np.zeros((B, 4))
+    xr[:, 0] = rng.uniform(-1, 1, B)
+    return ocp, ocp.params(x0, xr)
+
+
+@pytest.mark.parametrize("which", ["kin_bicycle", "dyn_bicycle", "cartpole"])
+def test_ode_plant_matches_oracle(mpcx, which):
+    from oracle import ode_ref
+
+    ocp, P = cases(which, 64, 10, seed=3)
+    pr = ode_ref.Problem(ocp)
+    rng = np.random.default_rng(4)
+    U = rng.uniform(ocp.u_lb, ocp.u_ub, (64, ocp.nu)) * 0.5
+    xf, qf = mpcx.integrator(ocp).batch(P, U)
+    ref = pr.F(P[:, :ocp.nx], U)
+    zr0 = np.stack([pr.refs(p)[0] for p in P])  # stage-0 reference of every instance
+    q = pr.l(np.concatenate([P[:, :ocp.nx], U], axis=1), zr0)
+    assert rel(xf, ref) <= 1e-12
+    assert rel(qf, q) <= 1e-12
+
+
+@pytest.mark.parametrize("which,N,B", [("kin_bicycle", 30, 6), ("dyn_bicycle", 20, 4), ("cartpole", 50, 6)])
+def test_ode_optimum_matches_oracle(mpcx, which, N, B):
+    from oracle import ode_ref
+
+    ocp, P = cases(which, B, N)
+    # tol 1e-10: at 1e-8 an interior point keeps ~1e-6 off active bounds on these less well scaled
+    # problems (kinematic bicycle: steering weight 0.05), and the check is of the fixed point
+    solver = mpcx.nlpsol("ode", "mi355x", ocp, {"ipopt": {"max_iter": 300, "tol": 1e-10}})
+    r = solver.solve_batch(P)
+    assert np.all(r["status"] == 0), r["status"]
+    pr = ode_ref.Problem(ocp)
+    for b in range(B):
+        X, U = pr.split_w(r["w"][b])
+        Uo, Xo, info = pr.solve(P[b], U0=U)  # started at the GPU point: same local optimum
+        assert info["status"] in ("converged", "stalled") and info["pg"] <= 1e-6, info
+        assert rel(U, Uo) <= U_TOL, (b, rel(U, Uo))
+        assert rel(X, Xo) <= U_TOL
+        assert abs(r["f"][b] - info["J"]) <= 1e-8 * max(1.0, abs(info["J"]))
+        kkt, gres = pr.kkt_residual(r["w"][b], r["lam_g"][b], r["lam_x"][b], P[b])
+        assert kkt <= 1e-6 and gres <= 1e-9, (b, kkt, gres)
+    if which == "dyn_bicycle":  # the vx >= 2.5 bound stays inactive (the oracle does not model it)
+        assert np.min(r["w"][:, 3::8]) > 2.6
+
+
+def test_cartpole_swingup_is_kkt_point(mpcx):
+    """Swing-up from hanging (phi = pi), N = 100: nonconvex, so the check is the oracle's KKT
+    residual at the GPU's primal-dual point (any local optimum of the NLP qualifies)."""
+    from oracle import ode_ref
+
+    ocp = mpcx.cartpole_swingup(N=100)
+    P = ocp.params(np.array([[0.0, 0.0, math.pi, 0.0], [0.5, 0.0, -math.pi + 0.1, 0.2]]), np.zeros(4))
+    solver = mpcx.nlpsol("swing", "mi355x", ocp, {"ipopt": {"max_iter": 1000, "tol": 1e-8}})
+    r = solver.solve_batch(P)
+    assert np.all(r["status"] == 0), r["status"]
+    pr = ode_ref.Problem(ocp)
+    for b in range(2):
+        kkt, gres = pr.kkt_residual(r["w"][b], r["lam_g"][b], r["lam_x"][b], P[b])
+        assert kkt <= 1e-6 and gres <= 1e-9, (b, kkt, gres)
+        _, U = pr.split_w(r["w"][b])
+        assert np.all(U >= -200 - 1e-9) and np.all(U <= 200 + 1e-9)
+
+
+@pytest.mark.parametrize("which,N", [("dyn_bicycle", 20), ("cartpole", 100)])
+def test_ode_run_equals_lockstep(mpcx, which, N):
+    """Multi-step launches == lock-step launches, bit for bit, for the ODE models too."""
+    import torch
+    from mpcx.device import DeviceLoop
+
+    ocp, P = cases(which, 32, N, seed=7)
+    solver = mpcx.nlpsol("s", "mi355x", ocp)
+    lock, run = DeviceLoop(solver, P), DeviceLoop(solver, P)
+    st_l, it_l = [], []
+    for _ in range(3):
+        lock.step()
+        torch.cuda.synchronize()
+        st_l.append(lock.status.cpu().numpy().copy())
+        it_l.append(lock.iters.cpu().numpy().copy())
+    st_r, it_r = run.run(3)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st_r.cpu().numpy(), np.array(st_l))
+    np.testing.assert_array_equal(it_r.cpu().numpy(), np.array(it_l))
+    assert np.all(np.array(st_l) == 0)
+    for n in ("P", "w", "w0", "lam", "lamx", "f"):
+        np.testing.assert_array_equal(getattr(run, n).cpu().numpy(), getattr(lock, n).cpu().numpy(), err_msg=n)

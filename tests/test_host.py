@@ -51,7 +51,8 @@ def test_python_binding_matches_header():
 
     assert set(mpcx._lib.EXPORTS) == set(declared_symbols())
     # struct layout: 8 int32 + 2 double + 6 x double[8] + 3 double (warm start) + 2 int32 (nx, nu)
-    assert ctypes.sizeof(mpcx._lib.Spec) == 8 * 4 + 2 * 8 + 6 * 8 * 8 + 3 * 8 + 2 * 4
+    # + double[8] (par)
+    assert ctypes.sizeof(mpcx._lib.Spec) == 8 * 4 + 2 * 8 + 6 * 8 * 8 + 3 * 8 + 2 * 4 + 8 * 8
 
 
 def test_default_spec_without_gpu(lib):
@@ -62,6 +63,12 @@ def test_default_spec_without_gpu(lib):
     assert s.N == 20 and s.M == 4 and abs(s.T - 0.2) < 1e-15 and s.max_iter == 2000
     assert list(s.Q[:3]) == [1.0, 5.0, 0.1] and list(s.R[:2]) == [0.5, 0.05]
     assert lib.mpcx_default_spec(ctypes.byref(s), 99, 20) < 0
+    # ODE models: dimensions, node cost and constants (include/mpcx.h mpcx_model)
+    for model, nx, nu, par in ((3, 3, 2, [0.5]), (4, 6, 2, [1200.0, 1.5, 2.0, 55000.0, 1350.0]),
+                               (5, 4, 1, [1.0, 1.0, 0.5, 9.81, 10.0])):
+        assert lib.mpcx_default_spec(ctypes.byref(s), model, 30) == 0
+        assert (s.nx, s.nu, s.cost, s.N) == (nx, nu, 1, 30)
+        assert list(s.par[:len(par)]) == par
 
 
 def test_no_cpu_fallback_when_gpu_missing():
