@@ -34,7 +34,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--N", type=int, default=20)
-    ap.add_argument("--model", choices=("unicycle", "pend"), default="unicycle")
+    ap.add_argument("--model", choices=("unicycle", "pend", "kin_bicycle", "dyn_bicycle", "cartpole"),
+                    default="unicycle")
     a = ap.parse_args()
     lib = mpcx._lib.load()
     lib.mpcx_diag_set_stamp_buffer.argtypes = [ctypes.c_void_p]
@@ -42,6 +43,18 @@ def main():
         lin = mpcx.inverted_pendulum_qp(N=a.N)
         solver = mpcx.nlpsol("stamps", "mi355x", lin)
         loop = DeviceLoop(solver, mpcx.lti.pendulum_params(lin, dist.config5_inputs(0, a.batch), 0.0))
+    elif a.model == "kin_bicycle":
+        solver = mpcx.nlpsol("stamps", "mi355x", mpcx.kinematic_bicycle_tracking(N=a.N))
+        loop = DeviceLoop(solver, dist.config3_bicycle_inputs(0, a.batch, N=a.N)[1])
+    elif a.model == "dyn_bicycle":
+        ocp = mpcx.dynamic_bicycle_lane_change(N=a.N)
+        solver = mpcx.nlpsol("stamps", "mi355x", ocp)
+        t0, x0, (X, Y, V) = dist.config4_bicycle_inputs(0, a.batch)
+        refs = np.stack([mpcx.ode.dyn_bicycle_references(X, Y, V, int(t), a.N) for t in t0])
+        loop = DeviceLoop(solver, ocp.params(x0, refs))
+    elif a.model == "cartpole":
+        solver = mpcx.nlpsol("stamps", "mi355x", mpcx.cartpole_swingup(N=a.N))
+        loop = DeviceLoop(solver, dist.config5_swingup_inputs(0, a.batch))
     else:
         solver = mpcx.nlpsol("stamps", "mi355x", mpcx.unicycle_point_to_point(N=a.N))
         loop = DeviceLoop(solver, dist.config2_inputs(0, a.batch))
