@@ -249,6 +249,24 @@ def load_traffic(B, N):
     return None
 
 
+def load_solve_pmc(kernel_substr):
+    """PMC characterisation of the solve kernel (tools/solve_pmc.sh -> profiles/), if committed."""
+    path = os.path.join(ROOT, "profiles", "r01_solve_kernel_pmc.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        for k, v in d.items():
+            if kernel_substr in k:
+                return {"kernel": k, "wave_cycles_share": v["wave_cycles_share"],
+                        "valu_active_share": v["valu_active_share"], "fp64_tflops": v.get("fp64_tflops"),
+                        "fp64_frac_of_peak": v.get("fp64_frac_of_peak"), "source": "profiles/r01_solve_kernel_pmc.json"}
+    except Exception:
+        return None
+    return None
+
+
 def main():
     args = parse()
     from mpcx import dist as mdist
@@ -436,11 +454,14 @@ def main():
     nw, ng, npar = solver._h.n_w, solver._h.n_g, solver._h.n_p
     io_bytes = B * 8 * ((npar + 2 * nw + ng) + (nw + 1 + ng + nw) + (ocp.nx + 2 * nw + ng)) + B * 8
     solve_info = {"kernel": "solve_kernel (fused IPM solve + plant/shift, one launch per step)",
-                  "bound": "latency: sequential Riccati/forward chains, one wave per SIMD",
+                  "bound": "VALU issue of each instance's serial instruction stream (sequential Riccati/forward "
+                           "chains run by the whole wave), one wave per SIMD",
                   "ms_p50": round(p50, 4), "iters_max_per_step_mean": round(float(lock_iters_max), 2),
                   "us_per_ipm_iteration": round(p50 * 1e3 / max(lock_iters_max, 1.0), 2),
                   "hbm_bytes_per_launch": io_bytes,
                   "hbm_frac": round(io_bytes / (p50 * 1e-3) / 1e9 / PEAK_HBM_GBS, 5)}
+    if cfg == 2 and variant is None:
+        solve_info["pmc"] = load_solve_pmc("UnicycleModel")
     if rank == 0:
         total = world * B * K
         out = {

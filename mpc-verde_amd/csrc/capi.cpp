@@ -37,6 +37,7 @@ struct mpcx_handle {
   int lin_ntab = 0, lin_rows = 0;
   const int32_t* ext_tab = nullptr;  // caller-owned device schedule (mpcx_set_linear_tab_dev)
   int ext_rows = 0;
+  int n_simd = 0;  // SIMDs of the device (CUs x 4): the solve launch widens lane groups to fill them
 };
 
 namespace {
@@ -289,6 +290,8 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
   HIPCHK(hipSetDevice(s->device));
   mpcx_handle* h = new mpcx_handle();
   h->spec = *s;
+  int n_cu = 0;
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess) h->n_simd = 4 * n_cu;
   h->spec.nx = nx_of(*s);
   h->spec.nu = nu_of(*s);
   const int nx = h->spec.nx, nz = nx + h->spec.nu;
@@ -397,6 +400,7 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
   mpcx::SolveArgs a{};
   a.B = B;
   a.model = h->spec.model;
+  a.n_simd = h->n_simd;
   a.nx = h->spec.nx;
   a.nu = h->spec.nu;
   a.lin.A = h->d_linA;

@@ -29,6 +29,7 @@ struct SolveArgs {
   int B, N, max_iter, p_layout;
   int p_stride;
   int model, nx, nu;
+  int n_simd;           // SIMDs of the device (0 = unknown): lane groups widen to fill them
   double tol;
   StageParams sp;       // unicycle constants
   LinTables lin;        // linear model tables

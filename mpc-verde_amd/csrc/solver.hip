@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 
 #include "collectives.h"
@@ -1120,8 +1121,17 @@ extern "C" int mpcx_diag_set_counter_buffer(void* d_buf) {
 // ---- launch helpers (called from capi.cpp) -----------------------------------
 template <class Model>
 static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
-  // lane group: the smallest power of two holding nodes 0..N; G > 64 spans G/64 waves
-  const int G = a.N < 16 ? 16 : a.N < 32 ? 32 : a.N < 64 ? 64 : a.N < 128 ? 128 : 256;
+  // lane group: the smallest power of two holding nodes 0..N; G > 64 spans G/64 waves.
+  // A batch too small to give every SIMD a wave gets wider groups (up to one instance per
+  // wave): the per-wave instruction stream is the same, but a wave then runs only its own
+  // instance's iterations, not the maximum over the instances it holds (config 2: +5 %
+  // solves/s in multi-step launches).  MPCX_MIN_GROUP forces a minimum (measurement knob).
+  int G = a.N < 16 ? 16 : a.N < 32 ? 32 : a.N < 64 ? 64 : a.N < 128 ? 128 : 256;
+  static const int min_group = [] {
+    const char* e = std::getenv("MPCX_MIN_GROUP");
+    return e ? std::atoi(e) : 0;
+  }();
+  while (G < 64 && (G < min_group || (long)a.B * G * 2 <= 64L * a.n_simd)) G *= 2;
   const long threads = (long)a.B * G;
   const int bs = G > 64 ? G : 64;
   const int blocks = (int)((threads + bs - 1) / bs);

@@ -1,0 +1,71 @@
+"""Summarise tools/solve_pmc.sh: per-dispatch averages over the solve_kernel dispatches.
+
+    python tools/solve_pmc_summary.py gpurun_out/solve_pmc > profiles/r01_solve_kernel_pmc.json
+
+SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles summed over waves
+(MI355X_MICROARCH.md, PMC units); WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES.
+FP64 lane-operations = 64 x (ADD + MUL + TRANS + 2 FMA) wave-instructions (inactive lanes
+included: an upper bound on useful flops).  Peak FP64 vector: 78.6 TFLOP/s (MI355X spec).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+PEAK_FP64_TFLOPS = 78.6
+
+
+def counters(d):
+    agg = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"]
+            if "solve_kernel" not in k:
+                continue
+            agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[k].add(r["Dispatch_Id"])
+    return {k: {c: v / len(disp[k]) for c, v in cs.items()} | {"dispatches": len(disp[k])} for k, cs in agg.items()}
+
+
+def durations(d):
+    out = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "solve_kernel" in r["Kernel_Name"]:
+                out[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    return out
+
+
+def main():
+    root = sys.argv[1]
+    a, b, tr = counters(os.path.join(root, "a")), counters(os.path.join(root, "b")), durations(os.path.join(root, "trace"))
+    res = {}
+    for k in a:
+        ca, cb = a[k], b.get(k, {})
+        ts = sorted(tr.get(k, []))
+        t = ts[len(ts) // 2] if ts else None
+        wc = ca["SQ_WAVE_CYCLES"]
+        f64 = {n: cb.get(f"SQ_INSTS_VALU_{n}_F64", 0.0) for n in ("ADD", "MUL", "FMA", "TRANS")}
+        flops = 64 * (f64["ADD"] + f64["MUL"] + f64["TRANS"] + 2 * f64["FMA"])
+        r = {"dispatches": ca["dispatches"], "duration_ms_median": None if t is None else round(t * 1e3, 4),
+             "wave_cycles_share": {"issuing": round(ca["SQ_ACTIVE_INST_ANY"] / wc, 4),
+                                   "dependency_or_pipe_stall": round(ca["SQ_WAIT_INST_ANY"] / wc, 4),
+                                   "waitcnt_or_barrier": round(ca["SQ_WAIT_ANY"] / wc, 4)},
+             "valu_active_share": round(ca["SQ_ACTIVE_INST_VALU"] / wc, 4),
+             "insts_per_dispatch": {"valu": ca["SQ_INSTS_VALU"], "salu": ca["SQ_INSTS_SALU"], "lds": ca["SQ_INSTS_LDS"]},
+             "f64_insts_per_dispatch": f64, "f64_lane_flops_per_dispatch": flops,
+             "valu_f64_share_of_valu": round(sum(f64.values()) / max(ca["SQ_INSTS_VALU"], 1.0), 4)}
+        if t:
+            r["fp64_tflops"] = round(flops / t / 1e12, 3)
+            r["fp64_frac_of_peak"] = round(flops / t / 1e12 / PEAK_FP64_TFLOPS, 4)
+            if cb.get("GRBM_GUI_ACTIVE"):
+                r["effective_clock_ghz"] = round(cb["GRBM_GUI_ACTIVE"] / 8 / t / 1e9, 3)
+        res[k] = r
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

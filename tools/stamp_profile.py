@@ -61,6 +61,9 @@ def main():
     for _ in range(a.steps):
         loop.step()
     G = 16 if a.N < 16 else 32 if a.N < 32 else 64 if a.N < 64 else 128 if a.N < 128 else 256
+    n_simd = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    while G < 64 and a.batch * G * 2 <= 64 * n_simd:  # launch_solve_model's widening rule
+        G *= 2
     waves = (a.batch * G + 63) // 64
     buf = torch.zeros(waves * 10, dtype=torch.int64, device="cuda")
     assert lib.mpcx_diag_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
