@@ -96,7 +96,8 @@ typedef struct mpcx_spec {
   int32_t M;            /* RK4 substeps per interval (M at :101; mpctools M at Trajectory_tracking.py:51) */
   int32_t max_iter;     /* IPOPT max_iter (:190) */
   int32_t device;       /* HIP device ordinal */
-  int32_t reserved;
+  int32_t group_policy; /* lanes per instance: 0 = widen (up to 64) while the batch leaves SIMDs idle,
+                           1 = the smallest power of two >= N+1 (same results either way) */
   double T;             /* sampling time (:31) */
   double tol;           /* IPOPT tol (default 1e-8) */
   double Q[8];          /* diagonal state weights (:78-83) */

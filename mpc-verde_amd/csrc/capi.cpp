@@ -274,6 +274,7 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
   if (s->param_layout != MPCX_P_X0_XREF && s->param_layout != MPCX_P_X0_STAGEREF)
     return fail(MPCX_EINVAL, "unknown param_layout");
   if (s->max_iter < 0) return fail(MPCX_EINVAL, "max_iter < 0");
+  if (s->group_policy != 0 && s->group_policy != 1) return fail(MPCX_EINVAL, "group_policy must be 0 or 1");
   if (!(s->tol > 0)) return fail(MPCX_EINVAL, "tol must be > 0");
   if (!(s->warm_mu_init > 0) || !(s->warm_bound_push > 0) || !(s->warm_mult_push > 0))
     return fail(MPCX_EINVAL, "warm_mu_init / warm_bound_push / warm_mult_push must be > 0");
@@ -401,6 +402,7 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
   a.B = B;
   a.model = h->spec.model;
   a.n_simd = h->n_simd;
+  a.group_policy = h->spec.group_policy;
   a.nx = h->spec.nx;
   a.nu = h->spec.nu;
   a.lin.A = h->d_linA;

@@ -30,6 +30,7 @@ struct SolveArgs {
   int p_stride;
   int model, nx, nu;
   int n_simd;           // SIMDs of the device (0 = unknown): lane groups widen to fill them
+  int group_policy;     // mpcx_spec.group_policy
   double tol;
   StageParams sp;       // unicycle constants
   LinTables lin;        // linear model tables

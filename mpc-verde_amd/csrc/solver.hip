@@ -20,7 +20,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
-#include <cstdlib>
 #include <cstdint>
 
 #include "collectives.h"
@@ -1125,13 +1124,10 @@ static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
   // A batch too small to give every SIMD a wave gets wider groups (up to one instance per
   // wave): the per-wave instruction stream is the same, but a wave then runs only its own
   // instance's iterations, not the maximum over the instances it holds (config 2: +5 %
-  // solves/s in multi-step launches).  MPCX_MIN_GROUP forces a minimum (measurement knob).
+  // solves/s in multi-step launches).  spec.group_policy = 1 keeps the narrowest group.
   int G = a.N < 16 ? 16 : a.N < 32 ? 32 : a.N < 64 ? 64 : a.N < 128 ? 128 : 256;
-  static const int min_group = [] {
-    const char* e = std::getenv("MPCX_MIN_GROUP");
-    return e ? std::atoi(e) : 0;
-  }();
-  while (G < 64 && (G < min_group || (long)a.B * G * 2 <= 64L * a.n_simd)) G *= 2;
+  if (a.group_policy == 0)
+    while (G < 64 && (long)a.B * G * 2 <= 64L * a.n_simd) G *= 2;
   const long threads = (long)a.B * G;
   const int bs = G > 64 ? G : 64;
   const int blocks = (int)((threads + bs - 1) / bs);

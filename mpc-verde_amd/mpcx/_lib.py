@@ -39,7 +39,7 @@ class Spec(ctypes.Structure):
 
     _fields_ = [("model", ctypes.c_int32), ("cost", ctypes.c_int32), ("param_layout", ctypes.c_int32),
                 ("N", ctypes.c_int32), ("M", ctypes.c_int32), ("max_iter", ctypes.c_int32),
-                ("device", ctypes.c_int32), ("reserved", ctypes.c_int32), ("T", ctypes.c_double),
+                ("device", ctypes.c_int32), ("group_policy", ctypes.c_int32), ("T", ctypes.c_double),
                 ("tol", ctypes.c_double), ("Q", ctypes.c_double * 8), ("R", ctypes.c_double * 8),
                 ("lbu", ctypes.c_double * 8), ("ubu", ctypes.c_double * 8), ("lbx", ctypes.c_double * 8),
                 ("ubx", ctypes.c_double * 8), ("warm_mu_init", ctypes.c_double),

@@ -61,7 +61,9 @@ class Solver:
             ip.pop(k, None)
         if ip:
             raise ValueError(f"unsupported ipopt options: {sorted(ip)}")
-        self._h = _lib.Handle(to_spec(ocp, self.max_iter, self.tol, device))
+        # not a CasADi option: lanes per instance (0 = fill idle SIMDs, 1 = narrowest group; same results)
+        self.group_policy = int(opts.get("group_policy", 0))
+        self._h = _lib.Handle(to_spec(ocp, self.max_iter, self.tol, device, group_policy=self.group_policy))
         if ocp.model == "linear":
             self._h.set_linear_model(ocp)
         self._stats = {}

@@ -103,7 +103,7 @@ MODEL_IDS = {"unicycle": _lib.MODEL_UNICYCLE, "linear": _lib.MODEL_LINEAR, "kin_
              "dyn_bicycle": _lib.MODEL_DYN_BICYCLE, "cartpole": _lib.MODEL_CARTPOLE}
 
 
-def to_spec(ocp, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4)) -> _lib.Spec:
+def to_spec(ocp, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4), group_policy=0) -> _lib.Spec:
     """mpcx_spec of an :class:`OCP` (unicycle), :class:`mpcx.lti.LinearOCP` (linear model;
     its stage tables are uploaded separately by the solver, mpcx_set_linear_model) or
     :class:`mpcx.ode.OdeOCP` (nonlinear ODE models, constants in ``par``)."""
@@ -120,6 +120,7 @@ def to_spec(ocp, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4)) -> 
     s.T, s.tol = float(ocp.T), float(tol)
     s.warm_mu_init, s.warm_bound_push, s.warm_mult_push = (float(v) for v in warm)
     s.nx, s.nu = int(ocp.nx), int(ocp.nu)
+    s.group_policy = int(group_policy)
     big = 1e20
 
     def fin(v, default):

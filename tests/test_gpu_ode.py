@@ -82,14 +82,16 @@ def test_ode_plant_matches_oracle(mpcx, which):
     assert rel(qf, q) <= 1e-12
 
 
-@pytest.mark.parametrize("which,N,B", [("kin_bicycle", 30, 6), ("dyn_bicycle", 20, 4), ("cartpole", 50, 6)])
-def test_ode_optimum_matches_oracle(mpcx, which, N, B):
+@pytest.mark.parametrize("policy", [0, 1])
+@pytest.mark.parametrize("which,N,B", [("kin_bicycle", 30, 6), ("dyn_bicycle", 20, 4), ("cartpole", 50, 6),
+                                       ("kin_bicycle", 1, 5), ("cartpole", 15, 5), ("cartpole", 130, 3)])
+def test_ode_optimum_matches_oracle(mpcx, which, N, B, policy):
     from oracle import ode_ref
 
     ocp, P = cases(which, B, N)
     # tol 1e-10: at 1e-8 an interior point keeps ~1e-6 off active bounds on these less well scaled
     # problems (kinematic bicycle: steering weight 0.05), and the check is of the fixed point
-    solver = mpcx.nlpsol("ode", "mi355x", ocp, {"ipopt": {"max_iter": 300, "tol": 1e-10}})
+    solver = mpcx.nlpsol("ode", "mi355x", ocp, {"ipopt": {"max_iter": 300, "tol": 1e-10}, "group_policy": policy})
     r = solver.solve_batch(P)
     assert np.all(r["status"] == 0), r["status"]
     pr = ode_ref.Problem(ocp)

@@ -246,6 +246,21 @@ def test_horizons(mpcx, C, R, N):
     assert np.mean(ok) >= 0.9
 
 
+@pytest.mark.parametrize("N,B", [(10, 40), (20, 37), (40, 9), (100, 5)])
+def test_group_policy_same_results(mpcx, N, B):
+    """Lane-group widening (spec.group_policy 0, the default: up to one instance per wave while
+    SIMDs would idle) and the narrowest group (policy 1: 4/2 instances per wave at N=10/20) give
+    the same bits: the extra lanes add exact zeros / neutral values to every reduction.  Policy 1
+    is also how the narrow-group code paths stay covered at test batch sizes."""
+    ocp = mpcx.unicycle_point_to_point(N=N)
+    P = config2_batch(B, seed=N + 1)
+    r0 = mpcx.nlpsol("s", "mi355x", ocp).solve_batch(P)
+    r1 = mpcx.nlpsol("s", "mi355x", ocp, {"group_policy": 1}).solve_batch(P)
+    assert np.all(r0["status"] == 0)
+    for n in ("w", "f", "lam_g", "lam_x", "status", "iters"):
+        np.testing.assert_array_equal(r0[n], r1[n], err_msg=n)
+
+
 def test_max_iter_status(mpcx):
     ocp = mpcx.unicycle_point_to_point(N=10)
     solver = mpcx.nlpsol("s", "mi355x", ocp, {"ipopt": {"max_iter": 2}})
