@@ -79,11 +79,17 @@ class Solver:
     # ---------------------------------------------------------------- layout
     @property
     def n_w(self):
-        return self.ocp.N * 2 if self.ocp.formulation == "single_shooting" else self._h.n_w
+        return self.ocp.N * self.ocp.nu if self.ocp.formulation == "single_shooting" else self._h.n_w
 
     @property
     def n_g(self):
-        return self.ocp.N * 2 if self.ocp.formulation == "single_shooting" else self._h.n_g
+        return self.ocp.N * self._ss_ng if self.ocp.formulation == "single_shooting" else self._h.n_g
+
+    @property
+    def _ss_ng(self):
+        """Single shooting: g entries per node k = 1..N -- (x_k, y_k) for the unicycle
+        (``single_shooting_v2.py:115-158``), the whole state for the ODE models."""
+        return 2 if self.ocp.model == "unicycle" else self.ocp.nx
 
     @property
     def n_p(self):
@@ -170,24 +176,25 @@ class Solver:
         ubx = _vec(ubx, self.n_w, "ubx", math.inf)
         lbg = _vec(lbg, self.n_g, "lbg", 0.0 if not ss else -math.inf)
         ubg = _vec(ubg, self.n_g, "ubg", 0.0 if not ss else math.inf)
-        if ss and ocp.model != "unicycle":
-            raise ValueError("single shooting is mapped for the unicycle model only")
+        if ss and ocp.model == "linear":
+            raise ValueError("single shooting is mapped for the unicycle and ODE models (stage-invariant dynamics)")
         if ss:
             if np.any(np.isfinite(lbg)) or np.any(np.isfinite(ubg)):
                 raise ValueError("single shooting: only inactive (+-inf) bounds on g are supported")
         elif np.any(lbg != 0) or np.any(ubg != 0):
             raise ValueError("multiple shooting: g are the shooting equalities, lbg = ubg = 0 required")
-        N = ocp.N
+        N, nx, nu = ocp.N, ocp.nx, ocp.nu
+        nz = nx + nu
         l0 = lx0 = None
         if ss:  # decision = U; bounds on U map onto the U slots of the multiple-shooting w
             lbw = np.full(self._h.n_w, -1e20)
             ubw = np.full(self._h.n_w, 1e20)
             for k in range(N):
-                lbw[3 + 5 * k:5 + 5 * k] = lbx[2 * k:2 * k + 2]
-                ubw[3 + 5 * k:5 + 5 * k] = ubx[2 * k:2 * k + 2]
+                lbw[nx + nz * k:nx + nz * k + nu] = lbx[nu * k:nu * (k + 1)]
+                ubw[nx + nz * k:nx + nz * k + nu] = ubx[nu * k:nu * (k + 1)]
             w0 = None
             if x0 is not None:
-                U = _vec(x0, 2 * N, "x0").reshape(N, 2)
+                U = _vec(x0, nu * N, "x0").reshape(N, nu)
                 X = self._rollout(P[0], U)
                 w0 = np.concatenate([X[0]] + [np.concatenate([U[k], X[k + 1]]) for k in range(N)])[None, :]
         else:
@@ -205,24 +212,25 @@ class Solver:
         w = r["w"][0]
         lam_x = r["lam_x"][0]
         if ss:
-            U = np.stack([w[3 + 5 * k:5 + 5 * k] for k in range(N)]).reshape(-1)
-            Xs = np.stack([w[5 + 5 * k:8 + 5 * k] for k in range(N)])
-            g = Xs[:, 0:2].reshape(-1)
-            lx = np.concatenate([lam_x[3 + 5 * k:5 + 5 * k] for k in range(N)])
+            U = np.stack([w[nx + nz * k:nx + nz * k + nu] for k in range(N)]).reshape(-1)
+            Xs = np.stack([w[nx + nz * k + nu:nx + nz * (k + 1)] for k in range(N)])
+            g = Xs[:, 0:self._ss_ng].reshape(-1)
+            lx = np.concatenate([lam_x[nx + nz * k:nx + nz * k + nu] for k in range(N)])
             return {"x": U[:, None], "f": np.array([[r["f"][0]]]), "g": g[:, None],
-                    "lam_g": np.zeros((2 * N, 1)), "lam_x": lx[:, None], "lam_p": np.zeros((self._h.n_p, 1))}
+                    "lam_g": np.zeros((self.n_g, 1)), "lam_x": lx[:, None], "lam_p": np.zeros((self._h.n_p, 1))}
         return {"x": w[:, None], "f": np.array([[r["f"][0]]]), "g": r["g"][0][:, None],
                 "lam_g": r["lam_g"][0][:, None], "lam_x": lam_x[:, None], "lam_p": np.zeros((self._h.n_p, 1))}
 
     def _rollout(self, P, U):
-        N = self.ocp.N
-        X = [np.asarray(P[0:3], float)]
+        """X_{k+1} = F(X_k, U_k) on the plant kernel, stage k's references in the stage-0 slot."""
+        N, nx, nz = self.ocp.N, self.ocp.nx, self.ocp.nx + self.ocp.nu
+        X = [np.asarray(P[0:nx], float)]
         F = Integrator(self.ocp, handle=self._h)
         for k in range(N):
             p = np.array(P, float).copy()
-            p[0:3] = X[-1]
+            p[0:nx] = X[-1]
             if self.ocp.param == "x0_stageref":
-                p[3:8] = P[3 + 5 * k:8 + 5 * k]
+                p[nx:nx + nz] = P[nx + nz * k:nx + nz * (k + 1)]
             X.append(F(p, U[k])[0].reshape(-1))
         return np.array(X)
 

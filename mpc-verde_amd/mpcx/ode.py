@@ -59,6 +59,8 @@ class OdeOCP:
                 raise ValueError(f"{name}: expected {n} entries")
         if self.cost != "node":
             raise ValueError("ODE models use the node cost")
+        if self.formulation not in ("multiple_shooting", "single_shooting"):
+            raise ValueError(f"unknown formulation {self.formulation!r}")
 
     @property
     def nx(self):
@@ -157,8 +159,10 @@ def dyn_bicycle_references(X, Y, V, t, N, Delta=0.05, par=DYN_BICYCLE_PAR, w=8):
     return np.stack([X[k], Y[k], psi[k], V[k], np.zeros(N), r[k], delta[k], ax[k]], axis=-1)
 
 
-def cartpole_swingup(N=100, T=0.01, M=1, u_max=200.0):
-    """Config 5 variant: nonlinear cart-pole, p = [x0; x_ref]."""
+def cartpole_swingup(N=100, T=0.01, M=1, u_max=200.0, formulation="multiple_shooting"):
+    """Config 5 variant: nonlinear cart-pole, p = [x0; x_ref].  formulation="single_shooting" (the
+    BASELINE label): decision = U (N), g = X_1..X_N with +-inf bounds; solved through the same
+    multiple-shooting kernel (same optimum)."""
     inf = math.inf
     return OdeOCP(model="cartpole", N=N, T=T, M=M, Q=(1.44, 0.0, 1.0, 0.0), R=(1e-4,), u_lb=(-u_max,), u_ub=(u_max,),
-                  x_lb=(-inf,) * 4, x_ub=(inf,) * 4, par=CARTPOLE_PAR, param="x0_xref")
+                  x_lb=(-inf,) * 4, x_ub=(inf,) * 4, par=CARTPOLE_PAR, param="x0_xref", formulation=formulation)

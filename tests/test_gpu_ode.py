@@ -126,6 +126,25 @@ def test_cartpole_swingup_is_kkt_point(mpcx):
         assert np.all(U >= -200 - 1e-9) and np.all(U <= 200 + 1e-9)
 
 
+def test_cartpole_single_shooting_call(mpcx):
+    """BASELINE's "single-shooting" cart-pole: decision = U, g = X_1..X_N (+-inf), CasADi-shaped
+    call; same optimum as the oracle's independent single-shooting solve."""
+    from oracle import ode_ref
+
+    N = 40
+    ocp = mpcx.cartpole_swingup(N=N, formulation="single_shooting")
+    solver = mpcx.nlpsol("ss", "mi355x", ocp, {"ipopt": {"tol": 1e-10}})
+    p = [0.1, 0.0, 0.2, -0.1, 0.5, 0.0, 0.0, 0.0]
+    sol = solver(x0=[0.0] * N, lbx=-200.0, ubx=200.0, lbg=-math.inf, ubg=math.inf, p=p)
+    assert sol["x"].shape == (N, 1) and sol["g"].shape == (4 * N, 1) and sol["lam_x"].shape == (N, 1)
+    assert solver.stats()["success"]
+    pr = ode_ref.Problem(ocp)
+    U, X, info = pr.solve(np.array(p))
+    assert info["status"] == "converged"
+    assert rel(sol["x"][:, 0], U[:, 0]) <= U_TOL
+    assert rel(sol["g"][:, 0], X[1:].reshape(-1)) <= U_TOL
+
+
 @pytest.mark.parametrize("which,N", [("dyn_bicycle", 20), ("cartpole", 100)])
 def test_ode_run_equals_lockstep(mpcx, which, N):
     """Multi-step launches == lock-step launches, bit for bit, for the ODE models too."""
