@@ -57,6 +57,26 @@ int hipfail(hipError_t e, const char* where) {
     if (e_ != hipSuccess) return hipfail(e_, #expr);   \
   } while (0)
 
+// The handle's device is made current for the duration of a call and the caller's current
+// device restored on every return path (a PyTorch process on another device keeps its state).
+struct DeviceScope {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) err = hipSetDevice(dev);
+    if (prev == dev || err != hipSuccess) prev = -1;  // nothing to restore
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+};
+#define DEVICE_SCOPE(dev)                                           \
+  DeviceScope device_scope_(dev);                                   \
+  if (device_scope_.err != hipSuccess) return hipfail(device_scope_.err, "hipSetDevice")
+
 // (nx, nu) fixed by the model; the linear model takes them from the spec
 int nx_of(const mpcx_spec& s) {
   switch (s.model) {
@@ -288,7 +308,7 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0) return fail(MPCX_EHIP, "no HIP device available");
   if (s->device < 0 || s->device >= ndev) return fail(MPCX_EINVAL, "device ordinal out of range");
-  HIPCHK(hipSetDevice(s->device));
+  DEVICE_SCOPE(s->device);
   mpcx_handle* h = new mpcx_handle();
   h->spec = *s;
   int n_cu = 0;
@@ -317,7 +337,7 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
 
 void mpcx_destroy(mpcx_handle* h) {
   if (!h) return;
-  (void)hipSetDevice(h->spec.device);
+  DeviceScope device_scope_(h->spec.device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   dev_free(h->d_lbw);
   dev_free(h->d_ubw);
@@ -346,7 +366,7 @@ int mpcx_set_linear_model(mpcx_handle* h, int32_t n_tab, const double* A, const 
   const int nx = h->spec.nx, nu = h->spec.nu, nz = nx + nu, nh = nz * (nz + 1) / 2, N = h->spec.N;
   for (long i = 0; i < (long)tab_rows * N; ++i)
     if (tab[i] < 0 || tab[i] >= n_tab) return fail(MPCX_EINVAL, "table index out of range at " + std::to_string(i));
-  HIPCHK(hipSetDevice(h->spec.device));
+  DEVICE_SCOPE(h->spec.device);
   HIPCHK(hipStreamSynchronize(h->stream));  // no launch may still read the old tables
   free_linear(h);
   std::vector<double> cz((size_t)n_tab * nx, 0.0);
@@ -445,7 +465,7 @@ int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const dou
   if (B < 0) return fail(MPCX_EINVAL, "B < 0");
   if (B == 0) return 0;
   if (int r = check_model_ready(h, B)) return r;
-  HIPCHK(hipSetDevice(h->spec.device));
+  DEVICE_SCOPE(h->spec.device);
   mpcx::SolveArgs a = make_args(h, B, d_P, d_w0, d_lam_g0, d_lam_x0, h->d_lbw, h->d_ubw, d_w_out, d_f_out, d_lam_g,
                                 d_lam_x, d_status, d_iters);
   HIPCHK(mpcx::launch_solve(a, (hipStream_t)stream));
@@ -460,7 +480,7 @@ int mpcx_step_dev(mpcx_handle* h, int32_t B, double* d_P, double* d_w0, double* 
   if (flags & ~(MPCX_STEP_COLD | MPCX_STEP_PRIMAL_ONLY)) return fail(MPCX_EINVAL, "unknown flags");
   if (B == 0) return 0;
   if (int r = check_model_ready(h, B)) return r;
-  HIPCHK(hipSetDevice(h->spec.device));
+  DEVICE_SCOPE(h->spec.device);
   const bool cold = flags & MPCX_STEP_COLD;
   const bool duals = !cold && !(flags & MPCX_STEP_PRIMAL_ONLY);
   mpcx::SolveArgs a = make_args(h, B, d_P, cold ? nullptr : d_w0, duals ? d_lam_g0 : nullptr,
@@ -484,7 +504,7 @@ int mpcx_run_dev(mpcx_handle* h, int32_t B, int32_t K, double* d_P, double* d_w0
   if (d_tabseq && h->spec.model != MPCX_MODEL_LINEAR) return fail(MPCX_EINVAL, "d_tabseq needs a linear model");
   if (B == 0) return 0;
   if (int r = check_model_ready(h, B)) return r;
-  HIPCHK(hipSetDevice(h->spec.device));
+  DEVICE_SCOPE(h->spec.device);
   const bool cold = flags & MPCX_STEP_COLD;
   const bool duals = !(flags & MPCX_STEP_PRIMAL_ONLY) && (d_lam_g0 || d_lam_x0);
   mpcx::SolveArgs a = make_args(h, B, d_P, cold ? nullptr : d_w0, (duals && !cold) ? d_lam_g0 : nullptr,
@@ -510,7 +530,7 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
   if (B == 0) return 0;
   if (int r = check_bounds_vec(h, lbw, ubw)) return r;
   if (int r = check_model_ready(h, B)) return r;
-  HIPCHK(hipSetDevice(h->spec.device));
+  DEVICE_SCOPE(h->spec.device);
   if (int r = ensure(h, B)) return r;
   hipStream_t s = h->stream;
   const double* dl = h->d_lbw;
@@ -561,7 +581,7 @@ int mpcx_plant_step(mpcx_handle* h, int32_t B, const double* P, const double* u,
   if (!h || !P || !u || !xf) return fail(MPCX_EINVAL, "null argument");
   if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
   if (int r = check_model_ready(h, B)) return r;
-  HIPCHK(hipSetDevice(h->spec.device));
+  DEVICE_SCOPE(h->spec.device);
   hipStream_t s = h->stream;
   const int nx = h->spec.nx, nu = h->spec.nu;
   if (int r = ensure(h, B)) return r;
@@ -585,7 +605,7 @@ int mpcx_shift_dev(mpcx_handle* h, int32_t B, double* d_P, const double* d_w, do
   if ((d_lam_g == nullptr) != (d_lam_g0_next == nullptr) || (d_lam_x == nullptr) != (d_lam_x0_next == nullptr))
     return fail(MPCX_EINVAL, "multiplier shift needs both source and destination");
   if (int r = check_model_ready(h, B)) return r;
-  HIPCHK(hipSetDevice(h->spec.device));
+  DEVICE_SCOPE(h->spec.device);
   mpcx::SolveArgs a = make_args(h, B, d_P, nullptr, nullptr, nullptr, h->d_lbw, h->d_ubw, nullptr, nullptr, nullptr,
                                 nullptr, nullptr, nullptr);
   HIPCHK(mpcx::launch_shift(a, d_P, d_w, d_w0_next, d_lam_g, d_lam_g0_next, d_lam_x, d_lam_x0_next,
@@ -599,7 +619,7 @@ int mpcx_rk4_sens_dev(mpcx_handle* h, int32_t B, const double* d_X, const double
   if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
   if (h->spec.model != MPCX_MODEL_UNICYCLE || h->spec.param_layout != MPCX_P_X0_XREF)
     return fail(MPCX_EINVAL, "rk4_sens_dev: unicycle model with param_layout X0_XREF only");
-  HIPCHK(hipSetDevice(h->spec.device));
+  DEVICE_SCOPE(h->spec.device);
   HIPCHK(mpcx::launch_rk4_sens(B, h->spec.N, stage_params(h->spec), d_X, d_U, d_xr, d_J, (hipStream_t)stream));
   return 0;
 }
@@ -610,7 +630,7 @@ int mpcx_rk4_sens(mpcx_handle* h, int32_t B, const double* w, const double* P, d
   if (B <= 0) return B == 0 ? 0 : fail(MPCX_EINVAL, "B < 0");
   if (h->spec.model != MPCX_MODEL_UNICYCLE || h->spec.param_layout != MPCX_P_X0_XREF)
     return fail(MPCX_EINVAL, "rk4_sens: unicycle model with param_layout X0_XREF only");
-  HIPCHK(hipSetDevice(h->spec.device));
+  DEVICE_SCOPE(h->spec.device);
   const int N = h->spec.N;
   const long T = ((long)B + 63) / 64, Bp = T * 64;  // 64-instance tiles (mpcx_rk4_sens_dev layout)
   auto tix = [T](int stage, int F, int i, long b) {
