@@ -123,14 +123,16 @@ def dptr(a):
     """double* of a C-contiguous float64 ndarray (or None)."""
     if a is None:
         return None
-    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    if not isinstance(a, np.ndarray) or a.dtype != np.float64 or not a.flags["C_CONTIGUOUS"]:
+        raise TypeError("expected a C-contiguous float64 ndarray")
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
 
 
 def iptr(a):
     if a is None:
         return None
-    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
+    if not isinstance(a, np.ndarray) or a.dtype != np.int32 or not a.flags["C_CONTIGUOUS"]:
+        raise TypeError("expected a C-contiguous int32 ndarray")
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
 
 

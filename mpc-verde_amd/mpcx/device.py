@@ -25,6 +25,23 @@ def ctypes_void(p):
     return ctypes.c_void_p(p)
 
 
+def _check(t, name, dtype, shape, device):
+    """Every tensor handed to the kernels as a raw device pointer: right dtype, exact shape,
+    contiguous, on the loop's device.  A wrong one would be an out-of-bounds access or a host
+    pointer dereferenced by the GPU, so it is rejected here."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected dtype {dtype}, got {t.dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if t.device != device:
+        raise ValueError(f"{name}: must live on {device}, got {t.device}")
+    return t
+
+
 class DeviceLoop:
     """B independent MPC instances stepped on one GPU.
 
@@ -39,7 +56,13 @@ class DeviceLoop:
     def __init__(self, solver: Solver, P0, device="cuda", stream=None, cold_first=True, warm_duals=True):
         self.solver = solver
         self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("DeviceLoop needs a HIP device (torch 'cuda' device)")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         P0 = np.ascontiguousarray(np.asarray(P0, np.float64))
+        if P0.ndim != 2 or P0.shape[1] != solver._h.n_p:
+            raise ValueError(f"P0: expected (B, {solver._h.n_p}), got {P0.shape}")
         self.B = P0.shape[0]
         nw, ng = solver._h.n_w, solver._h.n_g
         z = lambda *s: torch.zeros(s, dtype=torch.float64, device=self.device)  # noqa: E731
@@ -62,8 +85,8 @@ class DeviceLoop:
         s = ctypes_void(self.stream.cuda_stream)
         w0 = None if self._cold else _ptr(self.w0)
         warm = self.warm_duals and not self._cold
-        st = self.status if status_out is None else status_out
-        it = self.iters if iters_out is None else iters_out
+        st = self.status if status_out is None else _check(status_out, "status_out", torch.int32, (self.B,), self.device)
+        it = self.iters if iters_out is None else _check(iters_out, "iters_out", torch.int32, (self.B,), self.device)
         _lib.check(lib.mpcx_solve_batch_dev(self.solver._h.ptr, self.B, _ptr(self.P), w0,
                                             _ptr(self.lam0) if warm else None, _ptr(self.lamx0) if warm else None,
                                             _ptr(self.w), _ptr(self.f), _ptr(self.lam), _ptr(self.lamx), _ptr(st),
@@ -82,8 +105,10 @@ class DeviceLoop:
         """Per-step stage references (tracking, param layout x0_stageref): refs is a
         (B, N*(nx+nu)) float64 device tensor copied into P[:, nx:] on the loop's stream
         (Trajectory_tracking.py:105-106 sets solver.par["p", k] each step)."""
+        nx = self.solver.ocp.nx
+        _check(refs, "refs", torch.float64, (self.B, self.P.shape[1] - nx), self.device)
         with torch.cuda.stream(self.stream):
-            self.P[:, self.solver.ocp.nx:].copy_(refs, non_blocking=True)
+            self.P[:, nx:].copy_(refs, non_blocking=True)
 
     def run(self, K, status_out=None, iters_out=None, Pseq=None, tabseq=None):
         """K closed-loop steps in ONE launch (mpcx_run_dev): each instance runs its own
@@ -94,18 +119,21 @@ class DeviceLoop:
         current ones).  Returns (status, iters)."""
         lib = _lib.load()
         s = ctypes_void(self.stream.cuda_stream)
-        st = status_out if status_out is not None else torch.zeros((K, self.B), dtype=torch.int32, device=self.device)
-        it = iters_out if iters_out is not None else torch.zeros((K, self.B), dtype=torch.int32, device=self.device)
-        assert st.shape == (K, self.B) and it.shape == (K, self.B) and st.dtype == it.dtype == torch.int32
+        K = int(K)
+        if K < 1:
+            raise ValueError("K must be >= 1")
+        z = lambda: torch.zeros((K, self.B), dtype=torch.int32, device=self.device)  # noqa: E731
+        st = z() if status_out is None else _check(status_out, "status_out", torch.int32, (K, self.B), self.device)
+        it = z() if iters_out is None else _check(iters_out, "iters_out", torch.int32, (K, self.B), self.device)
         if Pseq is not None:
-            assert Pseq.dtype == torch.float64 and Pseq.is_contiguous() and Pseq.shape == (K, self.B, self.P.shape[1])
+            _check(Pseq, "Pseq", torch.float64, (K, self.B, self.P.shape[1]), self.device)
         if tabseq is not None:
-            assert tabseq.dtype == torch.int32 and tabseq.is_contiguous() and tabseq.shape[:2] == (K, self.B)
+            _check(tabseq, "tabseq", torch.int32, (K, self.B, self.solver.ocp.N), self.device)
         flags = _lib.STEP_COLD if self._cold else 0
         if not self.warm_duals:
             flags |= _lib.STEP_PRIMAL_ONLY
         d = self.warm_duals
-        _lib.check(lib.mpcx_run_dev(self.solver._h.ptr, self.B, int(K), _ptr(self.P), _ptr(self.w0),
+        _lib.check(lib.mpcx_run_dev(self.solver._h.ptr, self.B, K, _ptr(self.P), _ptr(self.w0),
                                     _ptr(self.lam0) if d else None, _ptr(self.lamx0) if d else None, flags, _ptr(Pseq),
                                     _ptr(tabseq), _ptr(self.w), _ptr(self.f), _ptr(self.lam), _ptr(self.lamx), _ptr(st),
                                     _ptr(it), s))
@@ -122,7 +150,7 @@ class DeviceLoop:
             _lib.check(lib.mpcx_set_linear_tab_dev(self.solver._h.ptr, None, 0))
             self._tab = None
             return
-        assert tab.dtype == torch.int32 and tab.is_contiguous() and tab.shape[0] == self.B
+        _check(tab, "tab", torch.int32, (self.B, self.solver.ocp.N), self.device)
         self._tab = tab
         _lib.check(lib.mpcx_set_linear_tab_dev(self.solver._h.ptr, ctypes_void(tab.data_ptr()), self.B))
 
@@ -134,8 +162,8 @@ class DeviceLoop:
         s = ctypes_void(self.stream.cuda_stream)
         flags = _lib.STEP_COLD if self._cold else (0 if self.warm_duals else _lib.STEP_PRIMAL_ONLY)
         d = self.warm_duals
-        st = self.status if status_out is None else status_out
-        it = self.iters if iters_out is None else iters_out
+        st = self.status if status_out is None else _check(status_out, "status_out", torch.int32, (self.B,), self.device)
+        it = self.iters if iters_out is None else _check(iters_out, "iters_out", torch.int32, (self.B,), self.device)
         _lib.check(lib.mpcx_step_dev(self.solver._h.ptr, self.B, _ptr(self.P), _ptr(self.w0),
                                      _ptr(self.lam0) if d else None, _ptr(self.lamx0) if d else None, flags,
                                      _ptr(self.w), _ptr(self.f), _ptr(self.lam), _ptr(self.lamx), _ptr(st), _ptr(it),

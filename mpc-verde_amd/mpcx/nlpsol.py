@@ -116,6 +116,8 @@ class Solver:
         w0a = None
         if w0 is not None:
             w0a = np.ascontiguousarray(np.asarray(w0, np.float64).reshape(B, nw))
+        lbw = _vec(lbw, nw, "lbw")  # the library reads n_w entries of each
+        ubw = _vec(ubw, nw, "ubw")
         l0 = None if lam_g0 is None else np.ascontiguousarray(np.asarray(lam_g0, np.float64).reshape(B, ng))
         lx0 = None if lam_x0 is None else np.ascontiguousarray(np.asarray(lam_x0, np.float64).reshape(B, nw))
         w = np.empty((B, nw))
@@ -140,6 +142,8 @@ class Solver:
         w = np.ascontiguousarray(np.atleast_2d(np.asarray(w, np.float64)))
         P = np.ascontiguousarray(np.atleast_2d(np.asarray(P, np.float64)))
         B, N = w.shape[0], self.ocp.N
+        if w.shape[1] != self._h.n_w or P.shape != (B, self._h.n_p):
+            raise ValueError(f"rk4_sens: w (B, {self._h.n_w}) and P (B, {self._h.n_p}) expected")
         c = np.empty((B, N, 3))
         q = np.empty((B, N))
         A = np.empty((B, N, 3, 3))
@@ -256,6 +260,8 @@ class Integrator:
         U = np.ascontiguousarray(np.atleast_2d(np.asarray(U, np.float64)))
         B = P.shape[0]
         nx, nu = self.ocp.nx, self.ocp.nu
+        if P.shape[1] != self._h.n_p:
+            raise ValueError(f"P must be (B, {self._h.n_p})")
         if U.shape != (B, nu):
             raise ValueError(f"U must be (B, {nu})")
         xf = np.empty((B, nx))

@@ -281,6 +281,29 @@ def test_invalid_arguments(mpcx):
         bad.N = n_bad
         with pytest.raises(mpcx._lib.MpcxError):
             mpcx.nlpsol("s", "mi355x", bad)
+    # buffers the library would read or write past their end are rejected before the call
+    P = np.zeros((2, 6))
+    with pytest.raises(ValueError):
+        solver.solve_batch(P, lbw=np.zeros(10))
+    with pytest.raises(ValueError):
+        mpcx.integrator(mpcx.unicycle_point_to_point(N=10)).batch(np.zeros((2, 5)), np.zeros((2, 2)))
+    with pytest.raises(ValueError):
+        solver.rk4_sens(np.zeros((2, 40)), P)
+    import torch
+    from mpcx.device import DeviceLoop
+
+    loop = DeviceLoop(solver, P + [0, 0, 0, 10, 10, 0])
+    with pytest.raises(ValueError):  # too short
+        loop.step(status_out=torch.zeros(1, dtype=torch.int32, device=loop.device))
+    with pytest.raises(TypeError):  # wrong dtype
+        loop.step(iters_out=torch.zeros(2, dtype=torch.int64, device=loop.device))
+    with pytest.raises(ValueError):  # host memory
+        loop.run(2, Pseq=torch.zeros((2, 2, 6), dtype=torch.float64))
+    with pytest.raises(ValueError):
+        loop.set_stage_refs(torch.zeros((2, 2), dtype=torch.float64, device=loop.device))
+    loop.step()
+    torch.cuda.synchronize()
+    assert np.all(loop.status.cpu().numpy() == 0)
 
 
 def test_single_shooting_formulation(mpcx, R, golden):
