@@ -210,7 +210,7 @@ def sweep_roofline(solver, torch, B, N, reps, stream):
     U = torch.empty((N, T, 2, 64), dtype=torch.float64).uniform_(-0.78, 0.78, generator=g)
     XR = torch.empty((1, T, 3, 64), dtype=torch.float64).uniform_(-10, 10, generator=g)
     X, U, XR = X.to(dev), U.to(dev), XR.to(dev)
-    J = torch.empty((N, T, 24, 64), dtype=torch.float64, device=dev)  # per-interval records
+    J = torch.empty((N, T, 12, 64, 2), dtype=torch.float64, device=dev)  # per-interval records (field pairs)
     lib = _lib.load()
     vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     s = ctypes.c_void_p(stream.cuda_stream)

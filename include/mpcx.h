@@ -233,8 +233,10 @@ int mpcx_rk4_sens(mpcx_handle* h, int32_t B, const double* w, const double* P, d
    tiles of 64; an array with S stages and F fields per stage holds element
    (stage s, field i, instance b) at  ((s*T + b/64)*F + i)*64 + b%64  (size S*T*F*64):
  *   d_X  S=N+1, F=nx;  d_U  S=N, F=nu;  d_xr  S=1, F=nx          (inputs)
- *   d_J  S=N, F=24: the per-interval record, fields
- *        0-2 c (defect), 3 q, 4-12 A (row-major), 13-18 Bm (row-major), 19-23 gq  (output) */
+ *   d_J  S=N, 24 fields per interval: 0-2 c (defect), 3 q, 4-12 A (row-major),
+ *        13-18 Bm (row-major), 19-23 gq (output), stored as 12 field PAIRS so that a lane
+ *        writes 16 B: field f of (stage s, instance b) at
+ *        (((s*T + b/64)*12 + f/2)*64 + b%64)*2 + f%2   (size N*T*24*64) */
 int mpcx_rk4_sens_dev(mpcx_handle* h, int32_t B, const double* d_X, const double* d_U, const double* d_xr,
                       double* d_J, void* stream);
 

@@ -636,6 +636,10 @@ int mpcx_rk4_sens(mpcx_handle* h, int32_t B, const double* w, const double* P, d
   auto tix = [T](int stage, int F, int i, long b) {
     return (((size_t)stage * T + (b >> 6)) * F + i) * 64 + (b & 63);
   };
+  // d_J record: field f of (stage, instance) in the 16-B field-pair layout
+  auto jix = [T](int stage, int f, long b) {
+    return ((((size_t)stage * T + (b >> 6)) * 12 + (f >> 1)) * 64 + (b & 63)) * 2 + (f & 1);
+  };
   const size_t nX = (size_t)(N + 1) * 3 * Bp, nU = (size_t)N * 2 * Bp, nR = (size_t)3 * Bp;
   const size_t nJ = (size_t)N * 24 * Bp;
   const size_t total = nX + nU + nR + nJ;
@@ -668,11 +672,11 @@ int mpcx_rk4_sens(mpcx_handle* h, int32_t B, const double* w, const double* P, d
   for (int b = 0; b < B; ++b)
     for (int k = 0; k < N; ++k) {
       const size_t o = (size_t)b * N + k;
-      for (int i = 0; i < 3; ++i) c[o * 3 + i] = hJ[tix(k, 24, i, b)];
-      q[o] = hJ[tix(k, 24, 3, b)];
-      for (int i = 0; i < 9; ++i) A[o * 9 + i] = hJ[tix(k, 24, 4 + i, b)];
-      for (int i = 0; i < 6; ++i) Bm[o * 6 + i] = hJ[tix(k, 24, 13 + i, b)];
-      for (int i = 0; i < 5; ++i) gq[o * 5 + i] = hJ[tix(k, 24, 19 + i, b)];
+      for (int i = 0; i < 3; ++i) c[o * 3 + i] = hJ[jix(k, i, b)];
+      q[o] = hJ[jix(k, 3, b)];
+      for (int i = 0; i < 9; ++i) A[o * 9 + i] = hJ[jix(k, 4 + i, b)];
+      for (int i = 0; i < 6; ++i) Bm[o * 6 + i] = hJ[jix(k, 13 + i, b)];
+      for (int i = 0; i < 5; ++i) gq[o * 5 + i] = hJ[jix(k, 19 + i, b)];
     }
   return 0;
 }

@@ -11,6 +11,10 @@
 #include "solver.h"
 #include "unicycle.h"
 
+#ifndef MPCX_PSCAN_DEFAULT
+#define MPCX_PSCAN_DEFAULT false
+#endif
+
 namespace mpcx {
 
 // ------------------------------------------------------------------------------------
@@ -24,6 +28,8 @@ struct UnicycleModel {
   // the line search's first trial evaluates derivatives, not just values: accepted (the
   // usual case) it is the next iteration's evaluation, which is then skipped
   static constexpr bool kEvalInSearch = true;
+  // backward Riccati recursion as a log-depth scan (pscan.h) instead of N dependent steps
+  static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT;
   struct Ctx {
     double xr[3], ur[2];
   };
@@ -61,6 +67,7 @@ struct LinearModel {
   static constexpr unsigned long long AMASK = (NX * NX >= 64) ? ~0ull : ((1ull << (NX * NX)) - 1);
   static constexpr unsigned long long BMASK = (1ull << (NX * NU)) - 1;
   static constexpr bool kEvalInSearch = false;  // a value is one mat-vec: nothing to save
+  static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT;
   struct Ctx {
     const double *A, *B, *c, *W;
     double zr[NZ];

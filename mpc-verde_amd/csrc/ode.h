@@ -169,6 +169,7 @@ struct OdeModel {
   static constexpr unsigned long long AMASK = amask();
   static constexpr unsigned long long BMASK = (1ull << (NX * NU)) - 1;
   static constexpr bool kEvalInSearch = false;
+  static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT;
   struct Ctx {
     double zr[NZ];
   };

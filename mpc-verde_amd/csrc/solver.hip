@@ -25,6 +25,7 @@
 #include "collectives.h"
 #include "models.h"
 #include "ode.h"
+#include "pscan.h"
 #include "riccati.h"
 #include "solver.h"
 
@@ -34,7 +35,12 @@
 __device__ unsigned long long* g_mpcx_stamps = nullptr;
 // per-instance event counters (diagnostic build; indices at the kernel's `diag` array)
 __device__ int* g_mpcx_diag = nullptr;
+constexpr int kDiag = 9;  // counters per instance
 #define DIAG(i) (++diag[(i)])
+#define DIAG_IF(c, i) \
+  do {                \
+    if (c) ++diag[(i)]; \
+  } while (0)
 #define STAMP(p)                                                                \
   do {                                                                          \
     __builtin_amdgcn_sched_barrier(0);                                          \
@@ -51,6 +57,9 @@ __device__ int* g_mpcx_diag = nullptr;
   } while (0)
 #define DIAG(i) \
   do {          \
+  } while (0)
+#define DIAG_IF(c, i) \
+  do {                \
   } while (0)
 #endif
 
@@ -271,8 +280,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #ifdef MPCX_STAMPS
   // 0 regularised iterations, 1 extra factorisations, 2 backtracks, 3 barrier updates,
   // 4 fraction-to-boundary-limited steps (alpha_max < 1), 5 tiny steps, 6 filter rejections,
-  // 7 f-type (Armijo) acceptances
-  int diag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // 7 f-type (Armijo) acceptances, 8 factorisations by the sequential fallback of the scan
+  int diag[kDiag] = {};
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = 0;
   int st_ph = 9;
@@ -463,6 +472,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       printf("OPT it=%d k=%d fs=%g Ed=%g Ec=%g E0=%g sd=%g lam1=%g z1=%g\n", it, k, fs, Ed, Ec, E0, sd, lam1, z1);
 #endif
     if (__all(done && step == K - 1)) break;
+    // multi-step launches: a wave whose instances all just finished a step skips the rest of
+    // this pass (its Newton step would be discarded) and restarts at the step boundary
+    if (K > 1 && __all(done)) continue;
 
     STAMP(1);
     // ------------------------------------------------------------ barrier update
@@ -525,53 +537,141 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       // backward sweep: node N .. 0 (value function moves lane k+1 -> k)
       double P[NP], p[NX];
       bool okl = true;
-      {
-        const double dl = (k == N) ? 1.0 : 0.0;  // P_N = Sigma_x + delta, p_N = barrier gradient
+      bool seq = true;  // group-uniform: this instance needs the sequential recursion
+      if constexpr (Model::kParallelRiccati) {
+        // ---- log-depth associative scan of conditional value functions (pscan.h)
+        RElem<NX> e;
+        bool eok = true;
+        if (hasU) {
+          eok = relem_stage<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, e);
+        } else {
+          relem_identity<NX>(e);
+          if (hasX) {  // node N: terminal (0, 0, 0, Sigma_x + delta, barrier gradient)
+#pragma unroll
+            for (int i = 0; i < NX * NX; ++i) e.A[i] = 0.0;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+#pragma unroll
+              for (int j = i; j < NX; ++j) e.J[symix(i, j, NX)] = (i == j) ? sig[i] + delta : 0.0;
+              e.p[i] = gp[i];
+            }
+          }
+        }
+        constexpr int GW = G < 64 ? G : 64;  // lanes scanned per wave
+        const int kw = k & (GW - 1);
+        for (int d = 1; d < GW && d <= N; d <<= 1) {  // wave-uniform trip count
+          RElem<NX> o;
+          relem_fetch<NX>(e, o, d, min(lane + d, 63));
+          if (kw + d < GW) relem_combine<NX>(e, o);
+        }
+        if constexpr (G > 64) {  // complete each wave's suffixes with the next wave's, last wave first
+          const int wv = (int)(threadIdx.x >> 6);
+          for (int ph = XWave<G>::W - 2; ph >= 0; --ph) {
+            double* b = xw.cur();
+            if (wv == ph + 1 && lane == 0) {
+#pragma unroll
+              for (int i = 0; i < NP; ++i) b[i] = e.J[i];
+#pragma unroll
+              for (int i = 0; i < NX; ++i) b[NP + i] = e.p[i];
+            }
+            xw.sync();
+            if (wv == ph) {
+              const double* in = xw.prev();
+              double J2[NP], p2[NX];
+#pragma unroll
+              for (int i = 0; i < NP; ++i) J2[i] = in[i];
+#pragma unroll
+              for (int i = 0; i < NX; ++i) p2[i] = in[NP + i];
+              relem_finish<NX>(e, J2, p2);
+            }
+          }
+        }
+        // value function of node k+1, then ONE node-parallel Riccati step per lane: gains,
+        // inertia test and (P_k, p_k) as the sequential recursion would produce them
+        double Jn[NP + NX], nx_[NP + NX];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) Jn[i] = e.J[i];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) Jn[NP + i] = e.p[i];
+        group_next<G, NP + NX>(Jn, nx_, xw);
+        const double dl = (k == N) ? 1.0 : 0.0;
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
 #pragma unroll
           for (int j = i; j < NX; ++j) P[symix(i, j, NX)] = (i == j) ? dl * (sig[i] + delta) : 0.0;
           p[i] = dl * gp[i];
         }
-      }
-      if constexpr (G <= 64) {
-        for (int j = N - 1; j >= 0; --j) {
-          double Pin_[NP], pin_[NX];
+        double dev = 0.0, mag = 1.0;
+        if (hasU) {
+          okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, nx_, nx_ + NP, P, p, fac);
 #pragma unroll
-          for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
-#pragma unroll
-          for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
-          if (k == j) okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, Pin_, pin_, P, p, fac);
-        }
-      } else {  // wave by wave, N-side first; the value function crosses waves through LDS
-        const int wv = (int)(threadIdx.x >> 6);
-        for (int ph = XWave<G>::W - 1; ph >= 0; --ph) {
-          if (wv == ph) {
-            const double* in = xw.prev();  // (P, p) of node 64 (ph + 1), written last phase
-            const int jtop = 64 * ph + 63;
-            for (int j = min(N - 1, jtop); j >= 64 * ph; --j) {
-              double Pin_[NP], pin_[NX];
-#pragma unroll
-              for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
-#pragma unroll
-              for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
-              if (j == jtop && lane == 63) {
-#pragma unroll
-                for (int i = 0; i < NP; ++i) Pin_[i] = in[i];
-#pragma unroll
-                for (int i = 0; i < NX; ++i) pin_[i] = in[NP + i];
-              }
-              if (k == j) okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, Pin_, pin_, P, p, fac);
-            }
-            if (ph > 0 && lane == 0) {
-              double* out = xw.cur();
-#pragma unroll
-              for (int i = 0; i < NP; ++i) out[i] = P[i];
-#pragma unroll
-              for (int i = 0; i < NX; ++i) out[NP + i] = p[i];
-            }
+          for (int i = 0; i < NP; ++i) {
+            dev = fmax(dev, fabs(P[i] - e.J[i]));
+            mag = fmax(mag, fabs(P[i]));
           }
-          xw.sync();
+#pragma unroll
+          for (int i = 0; i < NX; ++i) {
+            dev = fmax(dev, fabs(p[i] - e.p[i]));
+            mag = fmax(mag, fabs(p[i]));
+          }
+        }
+        // scan usable: stage R positive definite, finite, and consistent with the step
+        const bool good = eok && dev <= 1e-8 * mag;  // false for NaN
+        seq = gmin<G>(good ? 1.0 : 0.0, xw) < 0.5;
+        DIAG_IF(seq && !done, 8);
+      }
+      if (__any(seq)) {  // sequential recursion (models without the scan, or its fallback)
+        if (seq) {
+          okl = true;
+          const double dl = (k == N) ? 1.0 : 0.0;  // P_N = Sigma_x + delta, p_N = barrier gradient
+#pragma unroll
+          for (int i = 0; i < NX; ++i) {
+#pragma unroll
+            for (int j = i; j < NX; ++j) P[symix(i, j, NX)] = (i == j) ? dl * (sig[i] + delta) : 0.0;
+            p[i] = dl * gp[i];
+          }
+        }
+        if constexpr (G <= 64) {
+          for (int j = N - 1; j >= 0; --j) {
+            double Pin_[NP], pin_[NX];
+#pragma unroll
+            for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
+            if (seq && k == j)
+              okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, Pin_, pin_, P, p, fac);
+          }
+        } else {  // wave by wave, N-side first; the value function crosses waves through LDS
+          const int wv = (int)(threadIdx.x >> 6);
+          for (int ph = XWave<G>::W - 1; ph >= 0; --ph) {
+            if (wv == ph) {
+              const double* in = xw.prev();  // (P, p) of node 64 (ph + 1), written last phase
+              const int jtop = 64 * ph + 63;
+              for (int j = min(N - 1, jtop); j >= 64 * ph; --j) {
+                double Pin_[NP], pin_[NX];
+#pragma unroll
+                for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
+                if (j == jtop && lane == 63) {
+#pragma unroll
+                  for (int i = 0; i < NP; ++i) Pin_[i] = in[i];
+#pragma unroll
+                  for (int i = 0; i < NX; ++i) pin_[i] = in[NP + i];
+                }
+                if (seq && k == j)
+                  okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, Pin_, pin_, P, p, fac);
+              }
+              if (ph > 0 && lane == 0) {
+                double* out = xw.cur();
+#pragma unroll
+                for (int i = 0; i < NP; ++i) out[i] = P[i];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) out[NP + i] = p[i];
+              }
+            }
+            xw.sync();
+          }
         }
       }
 #pragma unroll
@@ -890,7 +990,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   STAMP(9);
 #ifdef MPCX_STAMPS
   if (g_mpcx_diag && valid && k == 0)
-    for (int i = 0; i < 8; ++i) g_mpcx_diag[(size_t)inst * 8 + i] = diag[i];
+    for (int i = 0; i < kDiag; ++i) g_mpcx_diag[(size_t)inst * kDiag + i] = diag[i];
   if (g_mpcx_stamps && (threadIdx.x & 63) == 0) {
     const long wv = gid / 64;
     for (int i = 0; i < 10; ++i) g_mpcx_stamps[wv * 10 + i] = st_acc[i];
@@ -988,13 +1088,20 @@ constexpr int kRec = 24;  // fields of the per-stage sweep record
 __device__ __forceinline__ size_t tix(int stage, int F, int i, long b, long T) {
   return (((size_t)stage * T + (b >> 6)) * F + i) * 64 + (b & 63);
 }
+// record index of field PAIR j (fields 2j, 2j+1) in units of 16 B: inside a tile's 12 KB
+// block of one stage, lane b%64 owns 16 contiguous bytes of each 1 KB pair row
+__device__ __forceinline__ size_t jpix(int stage, int j, long b, long T) {
+  return (((size_t)stage * T + (b >> 6)) * (kRec / 2) + j) * 64 + (b & 63);
+}
 
 __global__ __launch_bounds__(256) void rk4_sens_kernel(int B, int N, StageParams sp, const double* __restrict__ X,
                                                        const double* __restrict__ U, const double* __restrict__ XR,
                                                        double* __restrict__ J) {
+  typedef double v2d __attribute__((ext_vector_type(2)));
   const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const long T = ((long)B + 63) / 64;
+  v2d* __restrict__ J2 = reinterpret_cast<v2d*>(J);
   double x[3], xr[3];
   const double ur[2] = {0.0, 0.0};
   const double lz[3] = {0, 0, 0};
@@ -1011,17 +1118,24 @@ __global__ __launch_bounds__(256) void rk4_sens_kernel(int B, int N, StageParams
     for (int i = 0; i < 2; ++i) u[i] = U[tix(k, 2, i, b, T)];
     double xf[3], q, A[9], Bm[6], g[5], H[15];
     uni_derivs<false>(sp, x, u, xr, ur, lz, 1.0, xf, q, A, Bm, g, H);
-    // one 24-field record per stage: c(3) q(1) A(9) B(6) grad q(5) -- a wave's whole
+    // one 24-field record per stage: c(3) q(1) A(9) B(6) grad q(5), stored as 12 field
+    // pairs of 16 B per lane (1 KB per wave-instruction, nontemporal) -- a wave's whole
     // output of a stage is one contiguous 12 KB block
+    double r[kRec];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) __builtin_nontemporal_store(xf[i] - xn[i], &J[tix(k, kRec, i, b, T)]);
-    __builtin_nontemporal_store(q, &J[tix(k, kRec, 3, b, T)]);
+    for (int i = 0; i < 3; ++i) r[i] = xf[i] - xn[i];
+    r[3] = q;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) __builtin_nontemporal_store(A[i], &J[tix(k, kRec, 4 + i, b, T)]);
+    for (int i = 0; i < 9; ++i) r[4 + i] = A[i];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) __builtin_nontemporal_store(Bm[i], &J[tix(k, kRec, 13 + i, b, T)]);
+    for (int i = 0; i < 6; ++i) r[13 + i] = Bm[i];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(g[i], &J[tix(k, kRec, 19 + i, b, T)]);
+    for (int i = 0; i < 5; ++i) r[19 + i] = g[i];
+#pragma unroll
+    for (int j = 0; j < kRec / 2; ++j) {
+      const v2d v = {r[2 * j], r[2 * j + 1]};
+      __builtin_nontemporal_store(v, &J2[jpix(k, j, b, T)]);
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) x[i] = xn[i];
   }

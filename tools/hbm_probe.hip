@@ -96,6 +96,68 @@ __global__ void sweep_copy(const double* __restrict__ X, const double* __restric
     x2 = n2;
   }
 }
+
+// as sweep_copy, but the 24-field record is stored as 12 field pairs: lane writes 16 B
+// (fields 2j, 2j+1) at ((stage*T + tile)*12 + j)*64 + lane, i.e. 1 KB per wave-instruction
+template <bool NT>
+__global__ void sweep_copy16(const double* __restrict__ X, const double* __restrict__ U, double* __restrict__ J, int B,
+                             int S) {
+  const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const long T = (B + 63) / 64;
+  double x0 = X[ptix(0, 3, 0, b, T)], x1 = X[ptix(0, 3, 1, b, T)], x2 = X[ptix(0, 3, 2, b, T)];
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  v2d* J2 = reinterpret_cast<v2d*>(J);
+  for (int k = 0; k < S; ++k) {
+    const double n0 = X[ptix(k + 1, 3, 0, b, T)], n1 = X[ptix(k + 1, 3, 1, b, T)], n2 = X[ptix(k + 1, 3, 2, b, T)];
+    const double u0 = U[ptix(k, 2, 0, b, T)], u1 = U[ptix(k, 2, 1, b, T)];
+    const double base = x0 + x1 + x2 + u0 + u1;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      v2d v = {base + 2 * j, base + 2 * j + 1};
+      v2d* p = &J2[ptix(k, 12, j, b, T)];
+      if (NT) __builtin_nontemporal_store(v, p);
+      else *p = v;
+    }
+    x0 = n0;
+    x1 = n1;
+    x2 = n2;
+  }
+}
+
+// flat stage-parallel form: one thread per (instance, stage); block order = output order
+// (stage-major, 4 tiles of one stage per 256-thread block), so the write front sweeps
+// memory linearly as blocks are dispatched.  x_{k+1} is read by two threads (stages k, k+1).
+template <int W, bool NT>
+__global__ void sweep_flat(const double* __restrict__ X, const double* __restrict__ U, double* __restrict__ J, int B,
+                           int S) {
+  const long T = (B + 63) / 64;
+  const long tpb = blockDim.x / 64;                 // tiles per block
+  const long bps = (T + tpb - 1) / tpb;             // blocks per stage
+  const int k = (int)(blockIdx.x / bps);
+  const long b = (blockIdx.x % bps) * blockDim.x + threadIdx.x;
+  if (k >= S || b >= B) return;
+  const double x0 = X[ptix(k, 3, 0, b, T)], x1 = X[ptix(k, 3, 1, b, T)], x2 = X[ptix(k, 3, 2, b, T)];
+  const double n0 = X[ptix(k + 1, 3, 0, b, T)], n1 = X[ptix(k + 1, 3, 1, b, T)], n2 = X[ptix(k + 1, 3, 2, b, T)];
+  const double u0 = U[ptix(k, 2, 0, b, T)], u1 = U[ptix(k, 2, 1, b, T)];
+  const double base = x0 + x1 + x2 + u0 + u1 + n0 * n1 * n2;
+  if (W == 8) {
+#pragma unroll
+    for (int f = 0; f < 24; ++f) {
+      if (NT) __builtin_nontemporal_store(base + f, &J[ptix(k, 24, f, b, T)]);
+      else J[ptix(k, 24, f, b, T)] = base + f;
+    }
+  } else {
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    v2d* J2 = reinterpret_cast<v2d*>(J);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      v2d v = {base + 2 * j, base + 2 * j + 1};
+      if (NT) __builtin_nontemporal_store(v, &J2[ptix(k, 12, j, b, T)]);
+      else J2[ptix(k, 12, j, b, T)] = v;
+    }
+  }
+}
 // per element of `a`: 1 read, ~4.5 writes (9 writes per 2 reads)
 __global__ void mix(const double2* __restrict__ a, double2* __restrict__ o, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -157,6 +219,24 @@ int main() {
     const double byc = (double)Bs * ((S + 1) * 3 * 8 + S * 2 * 8 + S * 24 * 8);
     timeit([&] { hipLaunchKernelGGL(sweep_copy, dim3(Bs / 256), dim3(256), 0, 0, X, U, J, Bs, S); }, byc,
            "sweep traffic without arithmetic (compulsory bytes)");
+    timeit([&] { hipLaunchKernelGGL(sweep_copy16<false>, dim3(Bs / 256), dim3(256), 0, 0, X, U, J, Bs, S); }, byc,
+           "sweep traffic without arithmetic, 16-B record stores (field pairs)");
+    timeit([&] { hipLaunchKernelGGL(sweep_copy16<true>, dim3(Bs / 256), dim3(256), 0, 0, X, U, J, Bs, S); }, byc,
+           "sweep traffic without arithmetic, 16-B nontemporal record stores");
+    timeit([&] { hipLaunchKernelGGL(sweep_copy16<true>, dim3(Bs / 64), dim3(64), 0, 0, X, U, J, Bs, S); }, byc,
+           "sweep traffic without arithmetic, 16-B nt record stores, 64-thread blocks");
+    const double byf = byc + (double)Bs * S * 3 * 8;  // x_{k+1} read twice
+    timeit([&] { hipLaunchKernelGGL((sweep_flat<8, false>), dim3(Bs / 256 * S), dim3(256), 0, 0, X, U, J, Bs, S); }, byc,
+           "flat (instance,stage) threads, 8-B stores (GB/s of compulsory bytes)");
+    timeit([&] { hipLaunchKernelGGL((sweep_flat<8, true>), dim3(Bs / 256 * S), dim3(256), 0, 0, X, U, J, Bs, S); }, byc,
+           "flat (instance,stage) threads, 8-B nt stores");
+    timeit([&] { hipLaunchKernelGGL((sweep_flat<16, false>), dim3(Bs / 256 * S), dim3(256), 0, 0, X, U, J, Bs, S); }, byc,
+           "flat (instance,stage) threads, 16-B stores");
+    timeit([&] { hipLaunchKernelGGL((sweep_flat<16, true>), dim3(Bs / 256 * S), dim3(256), 0, 0, X, U, J, Bs, S); }, byc,
+           "flat (instance,stage) threads, 16-B nt stores");
+    timeit([&] { hipLaunchKernelGGL((sweep_flat<16, true>), dim3(Bs / 64 * S), dim3(64), 0, 0, X, U, J, Bs, S); }, byc,
+           "flat (instance,stage) threads, 16-B nt stores, 64-thread blocks");
+    (void)byf;
     CK(hipFree(X));
     CK(hipFree(U));
     CK(hipFree(J));

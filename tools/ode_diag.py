@@ -22,7 +22,8 @@ from mpcx import dist as mdist  # noqa: E402
 from mpcx.device import DeviceLoop  # noqa: E402
 
 NAMES = ["regularised_iters", "extra_factorisations", "backtracks", "barrier_updates", "ftb_limited_steps",
-         "tiny_steps", "filter_rejections", "armijo_acceptances"]
+         "tiny_steps", "filter_rejections", "armijo_acceptances", "scan_fallbacks"]
+ND = len(NAMES)  # counters per instance (solver.hip kDiag)
 
 
 def main():
@@ -31,7 +32,7 @@ def main():
     S = int(sys.argv[3]) if len(sys.argv) > 3 else 6
     lib = mpcx._lib.load()
     lib.mpcx_diag_set_counter_buffer.argtypes = [ctypes.c_void_p]
-    buf = torch.zeros(B * 8, dtype=torch.int32, device="cuda")
+    buf = torch.zeros(B * ND, dtype=torch.int32, device="cuda")
     assert lib.mpcx_diag_set_counter_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
     refs = None
     if model == "kin_bicycle":
@@ -62,17 +63,17 @@ def main():
         torch.cuda.synchronize()
         its.append(loop.iters.cpu().numpy().copy())
         sts.append(loop.status.cpu().numpy().copy())
-        cnt.append(buf.cpu().numpy().reshape(B, 8).copy())
+        cnt.append(buf.cpu().numpy().reshape(B, ND).copy())
     its, sts, cnt = np.array(its), np.array(sts), np.array(cnt)
     out = {"model": model, "B": B, "steps": S, "iters_per_step_mean": its.mean(axis=1).round(2).tolist(),
            "iters_per_step_max": its.max(axis=1).tolist(), "failed_per_step": (sts > 1).sum(axis=1).tolist()}
-    fi, fc = its.ravel(), cnt.reshape(-1, 8)
+    fi, fc = its.ravel(), cnt.reshape(-1, ND)
     for label, m in (("iters<=10", fi <= 10), ("iters 11-50", (fi > 10) & (fi <= 50)), ("iters>50", fi > 50)):
         out[label] = {"n": int(m.sum()), **{NAMES[i]: round(float(fc[m, i].mean()), 2) if m.any() else None
-                                            for i in range(8)}}
+                                            for i in range(ND)}}
     worst = np.argsort(-its.ravel())[:16]
     out["worst"] = [{"step": int(w // B), "inst": int(w % B), "iters": int(fi[w]), "status": int(sts.ravel()[w]),
-                     **{NAMES[i]: int(fc[w, i]) for i in range(8)}} for w in worst[:8]]
+                     **{NAMES[i]: int(fc[w, i]) for i in range(ND)}} for w in worst[:8]]
     print(json.dumps(out, indent=1))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     np.savez(os.path.join(ROOT, "gpurun_out", f"ode_diag_{model}.npz"),
