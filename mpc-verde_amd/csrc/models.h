@@ -12,7 +12,10 @@
 #include "unicycle.h"
 
 #ifndef MPCX_PSCAN_DEFAULT
-#define MPCX_PSCAN_DEFAULT false
+#define MPCX_PSCAN_DEFAULT true
+#endif
+#ifndef MPCX_PSCAN_UNICYCLE
+#define MPCX_PSCAN_UNICYCLE false
 #endif
 
 namespace mpcx {
@@ -29,7 +32,7 @@ struct UnicycleModel {
   // usual case) it is the next iteration's evaluation, which is then skipped
   static constexpr bool kEvalInSearch = true;
   // backward Riccati recursion as a log-depth scan (pscan.h) instead of N dependent steps
-  static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT;
+  static constexpr bool kParallelRiccati = MPCX_PSCAN_UNICYCLE;
   struct Ctx {
     double xr[3], ur[2];
   };
@@ -67,7 +70,8 @@ struct LinearModel {
   static constexpr unsigned long long AMASK = (NX * NX >= 64) ? ~0ull : ((1ull << (NX * NX)) - 1);
   static constexpr unsigned long long BMASK = (1ull << (NX * NU)) - 1;
   static constexpr bool kEvalInSearch = false;  // a value is one mat-vec: nothing to save
-  static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT;
+  // log-depth Riccati scan (pscan.h) for NX <= 4; NX = 5 spills its scan temporaries
+  static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT && NX_ <= 4;
   struct Ctx {
     const double *A, *B, *c, *W;
     double zr[NZ];

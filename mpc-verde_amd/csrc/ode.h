@@ -169,7 +169,7 @@ struct OdeModel {
   static constexpr unsigned long long AMASK = amask();
   static constexpr unsigned long long BMASK = (1ull << (NX * NU)) - 1;
   static constexpr bool kEvalInSearch = false;
-  static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT;
+  static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT && NX <= 5;  // NX = 6: LDS buffer too large
   struct Ctx {
     double zr[NZ];
   };

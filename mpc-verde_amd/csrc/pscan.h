@@ -36,8 +36,29 @@ namespace mpcx {
 template <int NX>
 struct RElem {
   static constexpr int NP = NX * (NX + 1) / 2;
+  static constexpr int NE = NX * NX + 2 * NX + 2 * NP;  // doubles per element
+  // field offsets (element f of lane t lives at buf[f * stride + t] in LDS)
+  static constexpr int oA = 0, ob = NX * NX, oC = ob + NX, oJ = oC + NP, op = oJ + NP;
   double A[NX * NX], b[NX], C[NP], J[NP], p[NX];
 };
+
+// store lane t's element in the LDS scan buffer (structure of arrays: conflict-free)
+template <int NX>
+__device__ __forceinline__ void relem_store(const RElem<NX>& e, double* buf, int stride, int t) {
+  using E = RElem<NX>;
+#pragma unroll
+  for (int i = 0; i < NX * NX; ++i) buf[(E::oA + i) * stride + t] = e.A[i];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    buf[(E::ob + i) * stride + t] = e.b[i];
+    buf[(E::op + i) * stride + t] = e.p[i];
+  }
+#pragma unroll
+  for (int i = 0; i < E::NP; ++i) {
+    buf[(E::oC + i) * stride + t] = e.C[i];
+    buf[(E::oJ + i) * stride + t] = e.J[i];
+  }
+}
 
 // identity element (lanes past node N)
 template <int NX>
@@ -140,11 +161,18 @@ __device__ __forceinline__ void inv_nopiv(double* a) {
   }
 }
 
-// e1 <- e1 (x) e2  (e1 = i->j, e2 = j->k)
+// e1 <- e1 (x) e2 with e2 read from the LDS scan buffer (q = buf + partner lane, fields
+// `stride` apart): the partner never occupies registers, and the temporaries are ordered so
+// that at most four NX x NX blocks are live besides e1
 template <int NX>
-__device__ __forceinline__ void relem_combine(RElem<NX>& e1, const RElem<NX>& e2) {
+__device__ __forceinline__ void relem_combine_lds(RElem<NX>& e1, const double* q, int stride) {
+  using E = RElem<NX>;
+  auto A2 = [&](int i, int j) { return q[(E::oA + i * NX + j) * stride]; };
+  auto b2 = [&](int i) { return q[(E::ob + i) * stride]; };
+  auto C2 = [&](int i, int j) { return q[(E::oC + symix(i, j, NX)) * stride]; };
+  auto J2 = [&](int i, int j) { return q[(E::oJ + symix(i, j, NX)) * stride]; };
+  auto p2 = [&](int i) { return q[(E::op + i) * stride]; };
   auto C1 = [&](int i, int j) { return e1.C[symix(i, j, NX)]; };
-  auto J2 = [&](int i, int j) { return e2.J[symix(i, j, NX)]; };
   double Mi[NX * NX];
 #pragma unroll
   for (int i = 0; i < NX; ++i)
@@ -156,76 +184,69 @@ __device__ __forceinline__ void relem_combine(RElem<NX>& e1, const RElem<NX>& e2
       Mi[i * NX + j] = acc;
     }
   inv_nopiv<NX>(Mi);
-  // p, J first (they read the old A1, b1)
-  double T2[NX * NX], J2A1[NX * NX], v[NX];
+  {  // p, J (read the old A1, b1): T2 = Mi A1, J <- T2^T (J2 A1) + J1, p <- T2^T (p2 + J2 b1) + p1
+    double T2[NX * NX], J2A1[NX * NX], v[NX];
 #pragma unroll
-  for (int i = 0; i < NX; ++i)
+    for (int i = 0; i < NX; ++i) {
 #pragma unroll
-    for (int j = 0; j < NX; ++j) {
-      double t = 0.0, u = 0.0;
+      for (int j = 0; j < NX; ++j) {
+        double t = 0.0, u = 0.0;
 #pragma unroll
-      for (int m = 0; m < NX; ++m) {
-        t = fma(Mi[i * NX + m], e1.A[m * NX + j], t);
-        u = fma(J2(i, m), e1.A[m * NX + j], u);
+        for (int m = 0; m < NX; ++m) {
+          t = fma(Mi[i * NX + m], e1.A[m * NX + j], t);
+          u = fma(J2(i, m), e1.A[m * NX + j], u);
+        }
+        T2[i * NX + j] = t;
+        J2A1[i * NX + j] = u;
       }
-      T2[i * NX + j] = t;
-      J2A1[i * NX + j] = u;
+      double acc = p2(i);
+#pragma unroll
+      for (int m = 0; m < NX; ++m) acc = fma(J2(i, m), e1.b[m], acc);
+      v[i] = acc;
     }
 #pragma unroll
-  for (int i = 0; i < NX; ++i) {
-    double acc = e2.p[i];
+    for (int i = 0; i < NX; ++i) {
+      double acc = e1.p[i];
 #pragma unroll
-    for (int m = 0; m < NX; ++m) acc = fma(J2(i, m), e1.b[m], acc);
-    v[i] = acc;
-  }
+      for (int m = 0; m < NX; ++m) acc = fma(T2[m * NX + i], v[m], acc);
+      e1.p[i] = acc;
 #pragma unroll
-  for (int i = 0; i < NX; ++i) {
-    double acc = e1.p[i];
+      for (int j = i; j < NX; ++j) {
+        double a = e1.J[symix(i, j, NX)];
 #pragma unroll
-    for (int m = 0; m < NX; ++m) acc = fma(T2[m * NX + i], v[m], acc);
-    e1.p[i] = acc;
-#pragma unroll
-    for (int j = i; j < NX; ++j) {
-      double a = e1.J[symix(i, j, NX)];
-#pragma unroll
-      for (int m = 0; m < NX; ++m) a = fma(T2[m * NX + i], J2A1[m * NX + j], a);
-      e1.J[symix(i, j, NX)] = a;
+        for (int m = 0; m < NX; ++m) a = fma(T2[m * NX + i], J2A1[m * NX + j], a);
+        e1.J[symix(i, j, NX)] = a;
+      }
     }
   }
-  // T1 = A2 Mi; A, b, C
+  // T1 = A2 Mi; b <- T1 (b1 - C1 p2) + b2, A <- T1 A1, C <- (T1 C1) A2^T + C2
   double T1[NX * NX], w[NX];
 #pragma unroll
-  for (int i = 0; i < NX; ++i)
+  for (int i = 0; i < NX; ++i) {
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       double acc = 0.0;
 #pragma unroll
-      for (int m = 0; m < NX; ++m) acc = fma(e2.A[i * NX + m], Mi[m * NX + j], acc);
+      for (int m = 0; m < NX; ++m) acc = fma(A2(i, m), Mi[m * NX + j], acc);
       T1[i * NX + j] = acc;
     }
-#pragma unroll
-  for (int i = 0; i < NX; ++i) {
     double acc = e1.b[i];
 #pragma unroll
-    for (int m = 0; m < NX; ++m) acc = fma(-C1(i, m), e2.p[m], acc);
+    for (int m = 0; m < NX; ++m) acc = fma(-C1(i, m), p2(m), acc);
     w[i] = acc;
   }
-  double T1C1[NX * NX], An[NX * NX];
+  double T1C1[NX * NX];
 #pragma unroll
   for (int i = 0; i < NX; ++i) {
-    double bacc = e2.b[i];
+    double bacc = b2(i);
 #pragma unroll
     for (int m = 0; m < NX; ++m) bacc = fma(T1[i * NX + m], w[m], bacc);
     e1.b[i] = bacc;
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      double a = 0.0, cc = 0.0;
+      double cc = 0.0;
 #pragma unroll
-      for (int m = 0; m < NX; ++m) {
-        a = fma(T1[i * NX + m], e1.A[m * NX + j], a);
-        cc = fma(T1[i * NX + m], C1(m, j), cc);
-      }
-      An[i * NX + j] = a;
+      for (int m = 0; m < NX; ++m) cc = fma(T1[i * NX + m], C1(m, j), cc);
       T1C1[i * NX + j] = cc;
     }
   }
@@ -233,98 +254,24 @@ __device__ __forceinline__ void relem_combine(RElem<NX>& e1, const RElem<NX>& e2
   for (int i = 0; i < NX; ++i)
 #pragma unroll
     for (int j = i; j < NX; ++j) {
-      double acc = e2.C[symix(i, j, NX)];
+      double acc = C2(i, j);
 #pragma unroll
-      for (int m = 0; m < NX; ++m) acc = fma(T1C1[i * NX + m], e2.A[j * NX + m], acc);
+      for (int m = 0; m < NX; ++m) acc = fma(T1C1[i * NX + m], A2(j, m), acc);
       e1.C[symix(i, j, NX)] = acc;
     }
+  // A <- T1 A1 column by column (a column of A1 is dead once its new column is formed)
 #pragma unroll
-  for (int i = 0; i < NX * NX; ++i) e1.A[i] = An[i];
-}
-
-// (J, p) <- e1 (x) (0, 0, 0, J2, p2): a partial suffix completed by the full suffix of the
-// next wave (whose A, b, C vanish); only J and p are needed
-template <int NX>
-__device__ __forceinline__ void relem_finish(RElem<NX>& e1, const double* J2p, const double* p2) {
-  auto C1 = [&](int i, int j) { return e1.C[symix(i, j, NX)]; };
-  auto J2 = [&](int i, int j) { return J2p[symix(i, j, NX)]; };
-  double Mi[NX * NX];
-#pragma unroll
-  for (int i = 0; i < NX; ++i)
-#pragma unroll
-    for (int j = 0; j < NX; ++j) {
-      double acc = (i == j) ? 1.0 : 0.0;
-#pragma unroll
-      for (int m = 0; m < NX; ++m) acc = fma(C1(i, m), J2(m, j), acc);
-      Mi[i * NX + j] = acc;
-    }
-  inv_nopiv<NX>(Mi);
-  double T2[NX * NX], J2A1[NX * NX], v[NX];
-#pragma unroll
-  for (int i = 0; i < NX; ++i)
-#pragma unroll
-    for (int j = 0; j < NX; ++j) {
-      double t = 0.0, u = 0.0;
-#pragma unroll
-      for (int m = 0; m < NX; ++m) {
-        t = fma(Mi[i * NX + m], e1.A[m * NX + j], t);
-        u = fma(J2(i, m), e1.A[m * NX + j], u);
-      }
-      T2[i * NX + j] = t;
-      J2A1[i * NX + j] = u;
-    }
-#pragma unroll
-  for (int i = 0; i < NX; ++i) {
-    double acc = p2[i];
-#pragma unroll
-    for (int m = 0; m < NX; ++m) acc = fma(J2(i, m), e1.b[m], acc);
-    v[i] = acc;
-  }
-#pragma unroll
-  for (int i = 0; i < NX; ++i) {
-    double acc = e1.p[i];
-#pragma unroll
-    for (int m = 0; m < NX; ++m) acc = fma(T2[m * NX + i], v[m], acc);
-    e1.p[i] = acc;
-#pragma unroll
-    for (int j = i; j < NX; ++j) {
-      double a = e1.J[symix(i, j, NX)];
-#pragma unroll
-      for (int m = 0; m < NX; ++m) a = fma(T2[m * NX + i], J2A1[m * NX + j], a);
-      e1.J[symix(i, j, NX)] = a;
-    }
-  }
-}
-
-// partner element of lane `src` (ds_bpermute; d = 1 by DPP)
-template <int NX>
-__device__ __forceinline__ void relem_fetch(const RElem<NX>& e, RElem<NX>& o, int d, int src) {
-  if (d == 1) {  // wave-uniform
-#pragma unroll
-    for (int i = 0; i < NX * NX; ++i) o.A[i] = from_next(e.A[i]);
+  for (int j = 0; j < NX; ++j) {
+    double col[NX];
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
-      o.b[i] = from_next(e.b[i]);
-      o.p[i] = from_next(e.p[i]);
+      double a = 0.0;
+#pragma unroll
+      for (int m = 0; m < NX; ++m) a = fma(T1[i * NX + m], e1.A[m * NX + j], a);
+      col[i] = a;
     }
 #pragma unroll
-    for (int i = 0; i < RElem<NX>::NP; ++i) {
-      o.C[i] = from_next(e.C[i]);
-      o.J[i] = from_next(e.J[i]);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < NX * NX; ++i) o.A[i] = from_lane(e.A[i], src);
-#pragma unroll
-    for (int i = 0; i < NX; ++i) {
-      o.b[i] = from_lane(e.b[i], src);
-      o.p[i] = from_lane(e.p[i], src);
-    }
-#pragma unroll
-    for (int i = 0; i < RElem<NX>::NP; ++i) {
-      o.C[i] = from_lane(e.C[i], src);
-      o.J[i] = from_lane(e.J[i], src);
-    }
+    for (int i = 0; i < NX; ++i) e1.A[i * NX + j] = col[i];
   }
 }
 

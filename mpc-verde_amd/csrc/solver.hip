@@ -119,6 +119,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   const int k = (int)(gid & (G - 1));  // node of this lane
   // multi-wave groups (G > 64, one workgroup per instance) exchange through LDS
   __shared__ double xch[2 * XWave<G>::W * kXchStride];
+  // LDS buffer of the Riccati scan (pscan.h): one element per thread, structure of arrays
+  constexpr int kSBS = G > 64 ? G : 64;  // threads per block = field stride
+  __shared__ double sbuf[Model::kParallelRiccati ? RElem<NX>::NE * kSBS : 1];
   XWave<G> xw{xch, 0};
   const int inst = (int)(gid / G);
   const bool valid = inst < a.B;
@@ -557,34 +560,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
             }
           }
         }
-        constexpr int GW = G < 64 ? G : 64;  // lanes scanned per wave
-        const int kw = k & (GW - 1);
-        for (int d = 1; d < GW && d <= N; d <<= 1) {  // wave-uniform trip count
-          RElem<NX> o;
-          relem_fetch<NX>(e, o, d, min(lane + d, 63));
-          if (kw + d < GW) relem_combine<NX>(e, o);
-        }
-        if constexpr (G > 64) {  // complete each wave's suffixes with the next wave's, last wave first
-          const int wv = (int)(threadIdx.x >> 6);
-          for (int ph = XWave<G>::W - 2; ph >= 0; --ph) {
-            double* b = xw.cur();
-            if (wv == ph + 1 && lane == 0) {
-#pragma unroll
-              for (int i = 0; i < NP; ++i) b[i] = e.J[i];
-#pragma unroll
-              for (int i = 0; i < NX; ++i) b[NP + i] = e.p[i];
-            }
-            xw.sync();
-            if (wv == ph) {
-              const double* in = xw.prev();
-              double J2[NP], p2[NX];
-#pragma unroll
-              for (int i = 0; i < NP; ++i) J2[i] = in[i];
-#pragma unroll
-              for (int i = 0; i < NX; ++i) p2[i] = in[NP + i];
-              relem_finish<NX>(e, J2, p2);
-            }
-          }
+        // Hillis-Steele suffix scan over the whole group through the LDS buffer `sbuf`
+        // (partner = thread t + d; block-uniform trip count, two barriers per level)
+        const int t = (int)threadIdx.x;
+        for (int d = 1; d < G && d <= N; d <<= 1) {
+          relem_store<NX>(e, sbuf, kSBS, t);
+          __syncthreads();
+          if (k + d < G) relem_combine_lds<NX>(e, sbuf + t + d, kSBS);
+          __syncthreads();
         }
         // value function of node k+1, then ONE node-parallel Riccati step per lane: gains,
         // inertia test and (P_k, p_k) as the sequential recursion would produce them
