@@ -36,6 +36,11 @@ struct UnicycleModel {
   struct Ctx {
     double xr[3], ur[2];
   };
+  // Jacobian/Hessian operands of the Newton step live in the kernel's registers
+  static constexpr bool kTableJac = false, kTableHess = false;
+  __device__ __forceinline__ static const double* jacA(const Ctx&, const double* A) { return A; }
+  __device__ __forceinline__ static const double* jacB(const Ctx&, const double* B) { return B; }
+  __device__ __forceinline__ static const double* hessW(const Ctx&, const double* H) { return H; }
   __device__ __forceinline__ static void load_ctx(const ModelArgs& a, int inst, const double* P, int k, bool hasU, Ctx& c) {
     for (int i = 0; i < 3; ++i) c.xr[i] = 0.0;
     c.ur[0] = c.ur[1] = 0.0;
@@ -70,12 +75,22 @@ struct LinearModel {
   static constexpr unsigned long long AMASK = (NX * NX >= 64) ? ~0ull : ((1ull << (NX * NX)) - 1);
   static constexpr unsigned long long BMASK = (1ull << (NX * NU)) - 1;
   static constexpr bool kEvalInSearch = false;  // a value is one mat-vec: nothing to save
-  // log-depth Riccati scan (pscan.h) for NX <= 4; NX = 5 spills its scan temporaries
-  static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT && NX_ <= 4;
   struct Ctx {
     const double *A, *B, *c, *W;
     double zr[NZ];
   };
+  // Log-depth Riccati scan (pscan.h), and with it A, B and the stage Hessian 2 W read from the
+  // stage tables (global memory, cache-resident) instead of register copies held through the
+  // whole iteration, which leaves the registers to the scan (derivs then does not fill A, Bm,
+  // H).  Measured (one MI355X): config 4 (NX = 4, N = 50) 9.3 M solves/s sequential, 11.9 M
+  // scan with register tables, 12.6 M scan with table operands; config 5 (NX = 5, N = 100)
+  // 0.91 M sequential, 0.43 M / 0.87 M with the scan (its 65-double elements still spill), so
+  // NX = 5 keeps the sequential recursion and register tables.
+  static constexpr bool kScan = MPCX_PSCAN_DEFAULT && NX_ <= 4;
+  static constexpr bool kParallelRiccati = kScan, kTableJac = kScan, kTableHess = kScan;
+  __device__ __forceinline__ static const double* jacA(const Ctx& c, const double* A) { return kTableJac ? c.A : A; }
+  __device__ __forceinline__ static const double* jacB(const Ctx& c, const double* B) { return kTableJac ? c.B : B; }
+  __device__ __forceinline__ static const double* hessW(const Ctx& c, const double* H) { return kTableHess ? c.W : H; }
   __device__ __forceinline__ static void load_ctx(const ModelArgs& a, int inst, const double* P, int k, bool hasU, Ctx& c) {
     const int N = a.N;
     int j = 0;
@@ -114,17 +129,22 @@ struct LinearModel {
     double dz[NZ];
 #pragma unroll
     for (int i = 0; i < NZ; ++i) dz[i] = z[i] - c.zr[i];
+    if constexpr (!kTableJac) {
 #pragma unroll
-    for (int i = 0; i < NX * NX; ++i) A[i] = c.A[i];
+      for (int i = 0; i < NX * NX; ++i) A[i] = c.A[i];
 #pragma unroll
-    for (int i = 0; i < NX * NU; ++i) Bm[i] = c.B[i];
+      for (int i = 0; i < NX * NU; ++i) Bm[i] = c.B[i];
+    }
+    if constexpr (!kTableHess)
+#pragma unroll
+      for (int i = 0; i < NH; ++i) H[i] = 2.0 * fs * c.W[i];
 #pragma unroll
     for (int r = 0; r < NX; ++r) {
       double acc = c.c[r];
 #pragma unroll
-      for (int m = 0; m < NX; ++m) acc = fma(A[r * NX + m], z[m], acc);
+      for (int m = 0; m < NX; ++m) acc = fma(c.A[r * NX + m], z[m], acc);
 #pragma unroll
-      for (int l = 0; l < NU; ++l) acc = fma(Bm[r * NU + l], z[NX + l], acc);
+      for (int l = 0; l < NU; ++l) acc = fma(c.B[r * NU + l], z[NX + l], acc);
       xf[r] = acc;
     }
     double acc = 0.0;
@@ -137,8 +157,6 @@ struct LinearModel {
       acc = fma(dz[i], wi, acc);
     }
     q = acc;
-#pragma unroll
-    for (int i = 0; i < NH; ++i) H[i] = 2.0 * fs * c.W[i];
   }
 };
 

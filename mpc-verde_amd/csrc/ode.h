@@ -173,6 +173,10 @@ struct OdeModel {
   struct Ctx {
     double zr[NZ];
   };
+  static constexpr bool kTableJac = false, kTableHess = false;
+  __device__ __forceinline__ static const double* jacA(const Ctx&, const double* A) { return A; }
+  __device__ __forceinline__ static const double* jacB(const Ctx&, const double* B) { return B; }
+  __device__ __forceinline__ static const double* hessW(const Ctx&, const double* H) { return H; }
   __device__ __forceinline__ static void load_ctx(const ModelArgs& a, int inst, const double* P, int k, bool hasU, Ctx& c) {
 #pragma unroll
     for (int i = 0; i < NZ; ++i) c.zr[i] = 0.0;

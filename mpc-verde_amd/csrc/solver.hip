@@ -246,8 +246,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     Model::derivs(ma, ctx, zz, ln, fs, xf, qv, A, Bm, gq, Hs);
     const double m = hasU ? 1.0 : 0.0;
     qv *= m;
+    if constexpr (!Model::kTableHess)
 #pragma unroll
-    for (int i = 0; i < NH; ++i) Hs[i] *= m;
+      for (int i = 0; i < NH; ++i) Hs[i] *= m;
 #pragma unroll
     for (int i = 0; i < NZ; ++i) gq[i] *= m;
 #pragma unroll
@@ -397,8 +398,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         for (int i = 0; i < NX; ++i) lam[i] *= fs;
 #pragma unroll
         for (int i = 0; i < NZ; ++i) gq[i] *= fs;
+        if constexpr (!Model::kTableHess)
 #pragma unroll
-        for (int i = 0; i < NH; ++i) Hs[i] *= fs;
+          for (int i = 0; i < NH; ++i) Hs[i] *= fs;
         if (warm)
 #pragma unroll
           for (int i = 0; i < NZ; ++i) {
@@ -429,13 +431,13 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         for (int j = 0; j < NX; ++j)
 #pragma unroll
           for (int m = 0; m < NX; ++m)
-            if (Model::AMASK & (1ull << (m * NX + j))) rd[j] = fma(A[m * NX + j], ln[m], rd[j]);
+            if (Model::AMASK & (1ull << (m * NX + j))) rd[j] = fma(Model::jacA(ctx, A)[m * NX + j], ln[m], rd[j]);
 #pragma unroll
         for (int l = 0; l < NU; ++l) {
           double acc = gq[NX + l];
 #pragma unroll
           for (int m = 0; m < NX; ++m)
-            if (Model::BMASK & (1ull << (m * NU + l))) acc = fma(Bm[m * NU + l], ln[m], acc);
+            if (Model::BMASK & (1ull << (m * NU + l))) acc = fma(Model::jacB(ctx, Bm)[m * NU + l], ln[m], acc);
           rd[NX + l] = acc;
         }
       }
@@ -533,8 +535,13 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       if (!__any(need)) break;
       // node-parallel: stage Hessian + Sigma + delta (off the sequential path)
       double Hd[NH];
+      // stage Hessian (table-Hessian models: 2 fs W of the stage table; none at node N)
+      const double hsc = Model::kTableHess ? (hasU ? 2.0 * fs : 0.0) : 1.0;
+      const double* Hsrc = Model::hessW(ctx, Hs);
+      const double* Aop = Model::jacA(ctx, A);
+      const double* Bop = Model::jacB(ctx, Bm);
 #pragma unroll
-      for (int i = 0; i < NH; ++i) Hd[i] = Hs[i];
+      for (int i = 0; i < NH; ++i) Hd[i] = Model::kTableHess ? hsc * Hsrc[i] : Hsrc[i];
 #pragma unroll
       for (int i = 0; i < NZ; ++i) Hd[symix(i, i, NZ)] += sig[i] + delta;
       // backward sweep: node N .. 0 (value function moves lane k+1 -> k)
@@ -546,7 +553,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         RElem<NX> e;
         bool eok = true;
         if (hasU) {
-          eok = relem_stage<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, e);
+          eok = relem_stage<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, Aop, Bop, cdef, e);
         } else {
           relem_identity<NX>(e);
           if (hasX) {  // node N: terminal (0, 0, 0, Sigma_x + delta, barrier gradient)
@@ -586,7 +593,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         }
         double dev = 0.0, mag = 1.0;
         if (hasU) {
-          okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, nx_, nx_ + NP, P, p, fac);
+          okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, Aop, Bop, cdef, nx_, nx_ + NP, P, p, fac);
 #pragma unroll
           for (int i = 0; i < NP; ++i) {
             dev = fmax(dev, fabs(P[i] - e.J[i]));
@@ -622,7 +629,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
             for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
             if (seq && k == j)
-              okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, Pin_, pin_, P, p, fac);
+              okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p, fac);
           }
         } else {  // wave by wave, N-side first; the value function crosses waves through LDS
           const int wv = (int)(threadIdx.x >> 6);
@@ -643,7 +650,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
                   for (int i = 0; i < NX; ++i) pin_[i] = in[NP + i];
                 }
                 if (seq && k == j)
-                  okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, cdef, Pin_, pin_, P, p, fac);
+                  okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p, fac);
               }
               if (ph > 0 && lane == 0) {
                 double* out = xw.cur();
@@ -698,14 +705,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         double acc = cdef[r];
 #pragma unroll
         for (int l = 0; l < NU; ++l)
-          if (Model::BMASK & (1ull << (r * NU + l))) acc = fma(Bm[r * NU + l], kfk[l], acc);
+          if (Model::BMASK & (1ull << (r * NU + l))) acc = fma(Model::jacB(ctx, Bm)[r * NU + l], kfk[l], acc);
         ccl[r] = acc;
 #pragma unroll
         for (int m = 0; m < NX; ++m) {
-          double e = (Model::AMASK & (1ull << (r * NX + m))) ? A[r * NX + m] : 0.0;
+          double e = (Model::AMASK & (1ull << (r * NX + m))) ? Model::jacA(ctx, A)[r * NX + m] : 0.0;
 #pragma unroll
           for (int l = 0; l < NU; ++l)
-            if (Model::BMASK & (1ull << (r * NU + l))) e = fma(Bm[r * NU + l], Kk[l * NX + m], e);
+            if (Model::BMASK & (1ull << (r * NU + l))) e = fma(Model::jacB(ctx, Bm)[r * NU + l], Kk[l * NX + m], e);
           Acl[r * NX + m] = e;
         }
       }
