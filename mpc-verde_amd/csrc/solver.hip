@@ -544,6 +544,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       for (int i = 0; i < NH; ++i) Hd[i] = Model::kTableHess ? hsc * Hsrc[i] : Hsrc[i];
 #pragma unroll
       for (int i = 0; i < NZ; ++i) Hd[symix(i, i, NZ)] += sig[i] + delta;
+
       // backward sweep: node N .. 0 (value function moves lane k+1 -> k)
       double P[NP], p[NX];
       bool okl = true;
@@ -1245,6 +1246,13 @@ static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
 
 // model dispatch: unicycle, and the linear-model shapes the reference's QPs need
 // (4x1 lateral / cart-pole, 5x1 cart-pole with the previous input as a state).
+#ifdef MPCX_ONLY_UNICYCLE  // diagnostic builds (register-usage experiments): unicycle kernels only
+#define MPCX_DISPATCH(a, FN, ...)                                 \
+  do {                                                            \
+    if ((a).model == 1) return FN<UnicycleModel>(__VA_ARGS__);    \
+    return hipErrorInvalidValue;                                  \
+  } while (0)
+#else
 #define MPCX_DISPATCH(a, FN, ...)                                                                \
   do {                                                                                           \
     if ((a).model == 1) return FN<UnicycleModel>(__VA_ARGS__);                                   \
@@ -1255,6 +1263,7 @@ static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
     if ((a).model == 5) return FN<OdeModel<CartPole>>(__VA_ARGS__);                              \
     return hipErrorInvalidValue;                                                                 \
   } while (0)
+#endif
 
 hipError_t launch_solve(const SolveArgs& a, hipStream_t stream) { MPCX_DISPATCH(a, launch_solve_model, a, stream); }
 
