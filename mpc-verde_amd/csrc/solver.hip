@@ -35,7 +35,7 @@
 __device__ unsigned long long* g_mpcx_stamps = nullptr;
 // per-instance event counters (diagnostic build; indices at the kernel's `diag` array)
 __device__ int* g_mpcx_diag = nullptr;
-constexpr int kDiag = 9;  // counters per instance
+constexpr int kDiag = 10;  // counters per instance
 #define DIAG(i) (++diag[(i)])
 #define DIAG_IF(c, i) \
   do {                \
@@ -73,6 +73,7 @@ constexpr double kGammaTheta = 1e-5, kGammaPhi = 1e-8, kDeltaSw = 1.0, kSTheta =
 constexpr double kEtaPhi = 1e-8, kGammaAlpha = 0.05;
 constexpr double kDw0 = 1e-4, kDwMin = 1e-20, kDwMax = 1e40, kKwMinus = 1.0 / 3, kKwPlus = 8, kKwPlusBar = 100;
 constexpr double kBoundPush = 1e-2, kBoundFrac = 1e-2, kInfBound = 1e19;
+constexpr int kFilterResetTrigger = 5, kMaxFilterResets = 5;  // IPOPT filter_reset_trigger, max_filter_resets
 
 // interleaved reference layout w = [X_0 | U_0 X_1 | ... | U_{N-1} X_N]
 template <int NX, int NU>
@@ -270,6 +271,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   double dw_last = 0.0;
   double fth = 0, fph = 0;  // filter entry #k of my instance (a ring of G entries in the lanes)
   int nfilt = 0, fnext = 0;
+  // IPOPT's filter-reset heuristic: iterations in a row whose last rejected trial point was
+  // rejected by the filter alone, and resets so far in this solve
+  int frej = 0, nfreset = 0;
   int status = valid ? 2 : 0;
   bool done = !valid;
   int it = 0;        // iteration of this instance's current solve
@@ -284,7 +288,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #ifdef MPCX_STAMPS
   // 0 regularised iterations, 1 extra factorisations, 2 backtracks, 3 barrier updates,
   // 4 fraction-to-boundary-limited steps (alpha_max < 1), 5 tiny steps, 6 filter rejections,
-  // 7 f-type (Armijo) acceptances, 8 factorisations by the sequential fallback of the scan
+  // 7 f-type (Armijo) acceptances, 8 factorisations by the sequential fallback of the scan,
+  // 9 filter resets
   int diag[kDiag] = {};
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = 0;
@@ -351,6 +356,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       theta_max = theta_min = 0.0;
       dw_last = 0.0;
       nfilt = fnext = 0;
+      frej = nfreset = 0;
       status = 2;
       done = false;
       it = 0;
@@ -875,6 +881,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     bool accepted = !done && tinystep;
     bool ftype = tinystep;
     bool trial_fresh = false;  // accepted at the first trial, which evaluated derivatives
+    bool lastrej_f = false;    // the last rejected trial passed the sufficient decrease test but not the filter
     // switching condition alpha (-gd)^s_phi > delta theta^s_theta  <=>  alpha > sw_a with
     // sw_a = delta theta^s_theta / (-gd)^s_phi -- also the third term of alpha_min; one exp of
     // logs, loop-invariant over the trials
@@ -917,7 +924,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       const double inF = (k < nfilt && tht >= fth && pht >= fph) ? 1.0 : 0.0;
       const bool infilter = gmax<G>(inF, xw) > 0.5;
       if (searching) {
-        bool acc = isfinite(pht) && isfinite(tht) && tht <= theta_max && !infilter;
+        // sufficient decrease (switching condition + Armijo, or theta/phi decrease), then the
+        // filter -- IPOPT's order, which decides whether a rejection was the filter's
+        bool acc = isfinite(pht) && isfinite(tht) && tht <= theta_max;
         bool ft = false;
         if (acc) {
           const bool sw = gd < 0 && alpha > sw_a;
@@ -927,6 +936,12 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           } else {
             acc = tht <= (1.0 - kGammaTheta) * thk || pht <= phk - kGammaPhi * thk + 10.0 * kEps * fabs(phk);
           }
+        }
+        if (acc && infilter) {
+          acc = false;
+          lastrej_f = true;
+        } else if (!acc) {
+          lastrej_f = false;
         }
         if (searching && infilter) DIAG(6);
         if (acc) {
@@ -958,6 +973,18 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         }
         fnext = (fnext + 1) & (G - 1);
         nfilt = nfilt < G ? nfilt + 1 : G;
+      }
+      // filter reset (IPOPT filter_reset_trigger = 5, max_filter_resets = 5): the filter is
+      // cleared once the last rejection of 5 successive iterations was the filter's
+      if (lastrej_f) {
+        if (++frej >= kFilterResetTrigger && nfreset < kMaxFilterResets) {
+          nfilt = fnext = 0;
+          ++nfreset;
+          frej = 0;
+          DIAG(9);
+        }
+      } else {
+        frej = 0;
       }
 #pragma unroll
       for (int i = 0; i < NZ; ++i) z[i] = fma(alpha, dz[i], z[i]);

@@ -459,6 +459,7 @@ int solve_one(Instance& I, double* w, double* lam, int max_iter, double tol, int
   double mu = warm ? warm->mu_init : 0.1, tau = std::max(kTauMin, 1.0 - mu);
   const double mu_min = tol / 10;
   std::vector<std::pair<double, double>> filter;
+  int frej = 0, nfreset = 0;  // IPOPT filter_reset_trigger / max_filter_resets (5, 5)
   double theta0 = norm1(e.c);
   const double theta_max = 1e4 * std::max(1.0, theta0), theta_min = 1e-4 * std::max(1.0, theta0);
   double dw_last = 0.0;
@@ -552,7 +553,7 @@ int solve_one(Instance& I, double* w, double* lam, int max_iter, double tol, int
     double tiny = 0;
     for (int i = 0; i < nw; ++i) tiny = std::max(tiny, std::fabs(dw[i]) / (1.0 + std::fabs(w[i])));
     double alpha = amax;
-    bool accepted = false, ftype = false;
+    bool accepted = false, ftype = false, lastrej_f = false;
     if (tiny < 10 * kEps) {
       accepted = true;
       ftype = true;
@@ -565,17 +566,24 @@ int solve_one(Instance& I, double* w, double* lam, int max_iter, double tol, int
         evaluate(I, wt.data(), lam, false, et);
         double tht = norm1(et.c), pht = barrier_phi(I, wt.data(), et.f, mu);
         bool acc = std::isfinite(pht) && tht <= theta_max;
-        if (acc)
-          for (auto& fe : filter)
-            if (tht >= fe.first && pht >= fe.second) { acc = false; break; }
-        if (acc) {
+        if (acc) {  // sufficient decrease first, then the filter (IPOPT's order)
           const bool sw = gd < 0 && alpha * std::pow(-gd, kSPhi) > kDelta * std::pow(thk, kSTheta);
           if (thk <= theta_min && sw) {
             acc = pht - phk <= kEtaPhi * alpha * gd + 10 * kEps * std::fabs(phk);
             ftype = acc;
           } else {
             acc = tht <= (1 - kGammaTheta) * thk || pht <= phk - kGammaPhi * thk + 10 * kEps * std::fabs(phk);
+            ftype = false;
           }
+        }
+        bool infilter = false;
+        for (auto& fe : filter)
+          if (tht >= fe.first && pht >= fe.second) { infilter = true; break; }
+        if (acc && infilter) {
+          acc = false;
+          lastrej_f = true;
+        } else if (!acc) {
+          lastrej_f = false;
         }
         if (acc) { accepted = true; break; }
         alpha *= 0.5;
@@ -584,6 +592,15 @@ int solve_one(Instance& I, double* w, double* lam, int max_iter, double tol, int
     }
     if (!accepted) { status = 3; break; }
     if (!ftype) filter.emplace_back((1 - kGammaTheta) * thk, phk - kGammaPhi * thk);
+    if (lastrej_f) {  // filter reset heuristic
+      if (++frej >= 5 && nfreset < 5) {
+        filter.clear();
+        ++nfreset;
+        frej = 0;
+      }
+    } else {
+      frej = 0;
+    }
     // ---- update
     for (int i = 0; i < nw; ++i) w[i] += alpha * dw[i];
     for (int i = 0; i < ng; ++i) lam[i] += alpha * (lamNew[i] - lam[i]);
