@@ -31,6 +31,9 @@ struct UnicycleModel {
   // the line search's first trial evaluates derivatives, not just values: accepted (the
   // usual case) it is the next iteration's evaluation, which is then skipped
   static constexpr bool kEvalInSearch = true;
+  // second-order correction (IPOPT max_soc): not here -- the first trial's evaluation replaces
+  // the current point's derivatives, and config-2/3 solves do not reach it
+  static constexpr bool kSOC = false;
   // backward Riccati recursion as a log-depth scan (pscan.h) instead of N dependent steps
   static constexpr bool kParallelRiccati = MPCX_PSCAN_UNICYCLE;
   struct Ctx {
@@ -75,6 +78,7 @@ struct LinearModel {
   static constexpr unsigned long long AMASK = (NX * NX >= 64) ? ~0ull : ((1ull << (NX * NX)) - 1);
   static constexpr unsigned long long BMASK = (1ull << (NX * NU)) - 1;
   static constexpr bool kEvalInSearch = false;  // a value is one mat-vec: nothing to save
+  static constexpr bool kSOC = false;           // linear constraints: a full step never increases theta
   struct Ctx {
     const double *A, *B, *c, *W;
     double zr[NZ];

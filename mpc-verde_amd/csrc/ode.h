@@ -74,6 +74,7 @@ __device__ __forceinline__ HD tan(HD x) {
 // ---------------------------------------------------------------------------- dynamics
 struct KinBicycle {
   static constexpr int NX = 3, NU = 2;
+  static constexpr bool kSOC = false;
   static constexpr unsigned NLMASK = (1u << 2) | (1u << 3) | (1u << 4);  // psi, v, delta
   static constexpr unsigned INDEP = (1u << 0) | (1u << 1);               // f does not read X, Y
   template <class S>
@@ -86,6 +87,7 @@ struct KinBicycle {
 
 struct DynBicycle {
   static constexpr int NX = 6, NU = 2;
+  static constexpr bool kSOC = true;
   // psi, vx, vy, r, delta (ax enters linearly, X and Y not at all)
   static constexpr unsigned NLMASK = (1u << 2) | (1u << 3) | (1u << 4) | (1u << 5) | (1u << 6);
   static constexpr unsigned INDEP = (1u << 0) | (1u << 1);
@@ -109,6 +111,7 @@ struct DynBicycle {
 
 struct CartPole {
   static constexpr int NX = 4, NU = 1;
+  static constexpr bool kSOC = false;
   static constexpr unsigned NLMASK = (1u << 1) | (1u << 2) | (1u << 3) | (1u << 4);  // p', phi, phi', F
   static constexpr unsigned INDEP = (1u << 0);                                        // f does not read p
   template <class S>
@@ -169,6 +172,14 @@ struct OdeModel {
   static constexpr unsigned long long AMASK = amask();
   static constexpr unsigned long long BMASK = (1ull << (NX * NU)) - 1;
   static constexpr bool kEvalInSearch = false;
+  // IPOPT's second-order correction (solver.hip line search, max_soc = 4), per model where it
+  // measured better (one MI355X, bench --model): 6-state bicycle 24 k -> 105 k solves/s (lock-step
+  // 4 k -> 53 k; max iterations 651 -> 66; failed instance-steps 10 -> 2).  Not enabled: the
+  // kinematic bicycle (one config-3 instance then alternates SOC steps that trade feasibility
+  // for barrier objective until max_iter, 1.09 M -> 0.27 M solves/s in multi-step launches,
+  // though lock-step rises 0.47 M -> 2.19 M), the cart-pole (no gain; +14 % per iteration from
+  // the extra registers).
+  static constexpr bool kSOC = Dyn::kSOC;
   static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT && NX <= 5;  // NX = 6: LDS buffer too large
   struct Ctx {
     double zr[NZ];

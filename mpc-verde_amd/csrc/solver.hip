@@ -35,7 +35,7 @@
 __device__ unsigned long long* g_mpcx_stamps = nullptr;
 // per-instance event counters (diagnostic build; indices at the kernel's `diag` array)
 __device__ int* g_mpcx_diag = nullptr;
-constexpr int kDiag = 10;  // counters per instance
+constexpr int kDiag = 12;  // counters per instance
 #define DIAG(i) (++diag[(i)])
 #define DIAG_IF(c, i) \
   do {                \
@@ -289,7 +289,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   // 0 regularised iterations, 1 extra factorisations, 2 backtracks, 3 barrier updates,
   // 4 fraction-to-boundary-limited steps (alpha_max < 1), 5 tiny steps, 6 filter rejections,
   // 7 f-type (Armijo) acceptances, 8 factorisations by the sequential fallback of the scan,
-  // 9 filter resets
+  // 9 filter resets, 10 first trials rejected with increased infeasibility (SOC-eligible),
+  // 11 accepted second-order corrections
   int diag[kDiag] = {};
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = 0;
@@ -703,16 +704,18 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 
     STAMP(4);
     // ------------------------------------------------------------ forward sweep: dw (lane k-1 -> k)
-    {
+    // (a lambda: the second-order correction re-runs it with other right-hand sides)
+    auto forward = [&](const double* cc_, const double* kf_, const double* pv_, const double* c0v_, double* dzo_,
+                       double* dlo_) __attribute__((always_inline)) {
       // closed-loop map of the step, node-parallel (off the sequential chain):
       // dx_{k+1} = (A + B K) dx_k + (c + B k_f);  du_k = k_f + K dx_k afterwards
       double Acl[NX * NX], ccl[NX];
 #pragma unroll
       for (int r = 0; r < NX; ++r) {
-        double acc = cdef[r];
+        double acc = cc_[r];
 #pragma unroll
         for (int l = 0; l < NU; ++l)
-          if (Model::BMASK & (1ull << (r * NU + l))) acc = fma(Model::jacB(ctx, Bm)[r * NU + l], kfk[l], acc);
+          if (Model::BMASK & (1ull << (r * NU + l))) acc = fma(Model::jacB(ctx, Bm)[r * NU + l], kf_[l], acc);
         ccl[r] = acc;
 #pragma unroll
         for (int m = 0; m < NX; ++m) {
@@ -756,7 +759,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
           for (int i = 0; i < NX * NX; ++i) Am[i] = (k == 0) ? 0.0 : prv[i];
 #pragma unroll
-          for (int i = 0; i < NX; ++i) cm[i] = (k == 0) ? c0[i] : prv[NX * NX + i];
+          for (int i = 0; i < NX; ++i) cm[i] = (k == 0) ? c0v_[i] : prv[NX * NX + i];
         }
         const int kw = k & (GW - 1);  // position inside the wave
 #pragma unroll
@@ -813,31 +816,32 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           }
         }
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dz[i] = cm[i];
+        for (int i = 0; i < NX; ++i) dzo_[i] = cm[i];
       }
       // du_k = k_f + K dx_k on all lanes at once (the last node has no control)
 #pragma unroll
       for (int l = 0; l < NU; ++l) {
-        double acc = kfk[l];
+        double acc = kf_[l];
 #pragma unroll
-        for (int m = 0; m < NX; ++m) acc = fma(Kk[l * NX + m], dz[m], acc);
-        dz[NX + l] = (k < N) ? acc : 0.0;
+        for (int m = 0; m < NX; ++m) acc = fma(Kk[l * NX + m], dzo_[m], acc);
+        dzo_[NX + l] = (k < N) ? acc : 0.0;
       }
       // lambda+ = P_k dx_k + p_k (node-parallel, after the sequential sweep)
 #pragma unroll
       for (int i = 0; i < NX; ++i) {
-        double acc = pk[i];
+        double acc = pv_[i];
 #pragma unroll
-        for (int m = 0; m < NX; ++m) acc = fma(Pk[symix(i, m, NX)], dz[m], acc);
-        dlam[i] = acc - lam[i];
+        for (int m = 0; m < NX; ++m) acc = fma(Pk[symix(i, m, NX)], dzo_[m], acc);
+        dlo_[i] = acc - lam[i];
       }
       if (!hasX) {
 #pragma unroll
-        for (int i = 0; i < NZ; ++i) dz[i] = 0.0;
+        for (int i = 0; i < NZ; ++i) dzo_[i] = 0.0;
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dlam[i] = 0.0;
+        for (int i = 0; i < NX; ++i) dlo_[i] = 0.0;
       }
-    }
+    };
+    forward(cdef, kfk, pk, c0, dz, dlam);
 
     STAMP(5);
     // ------------------------------------------------------------ bound-dual step, fraction to boundary
@@ -864,7 +868,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         gd_l += gp[i] * dz[i];
       }
     }
-    const double amax = gmin<G>(amax_l, xw), az = gmin<G>(az_l, xw), tiny = gmax<G>(tiny_l, xw);
+    const double amax = gmin<G>(amax_l, xw), tiny = gmax<G>(tiny_l, xw);
+    double az = gmin<G>(az_l, xw);  // dual step length (a second-order correction replaces it)
     if (!done && amax < 1.0) DIAG(4);
     if (!done && tiny < 10.0 * kEps) DIAG(5);
     const double gd = gsum<G>(gd_l, xw);
@@ -888,6 +893,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     const double sw_a = gd < 0 ? exp(log(kDeltaSw) + kSTheta * log(thk) - kSPhi * log(-gd)) : 0.0;
     const double amin = gd < 0 ? kGammaAlpha * fmin(kGammaTheta, fmin(kGammaPhi * thk / (-gd), sw_a))
                                : kGammaAlpha * kGammaTheta;
+    if constexpr (!Model::kSOC) {
     for (int ls = 0; ls < 80; ++ls) {
       if (!__any(searching)) break;
       double zt[NZ];
@@ -956,6 +962,253 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           if (alpha < amin) searching = false;  // would need restoration
         }
       }
+    }
+    } else {  // models with the second-order correction (their trials evaluate values only)
+    // trial point zt: constraint violation, barrier objective, filter membership (group sums);
+    // ct / ct0 receive the trial's own constraint values (interval k, and g_0 on lane 0)
+    auto trial_value = [&](const double* zt, double& tht, double& pht, bool& infilter, double* ct, double* ct0)
+                           __attribute__((always_inline)) {
+      double xtn[NX];
+      group_next<G, NX>(zt, xtn, xw);
+      double xft[NX], qt;
+      Model::value(ma, ctx, zt, xft, qt);
+      double tht_l = 0, pht_l = 0;
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        ct[i] = hasU ? xft[i] - xtn[i] : 0.0;
+        ct0[i] = (valid && k == 0) ? x0[i] - zt[i] : 0.0;
+      }
+      if (hasU) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) tht_l += fabs(ct[i]);
+        pht_l = fs * qt;
+      }
+      if (valid && k == 0)
+#pragma unroll
+        for (int i = 0; i < NX; ++i) tht_l += fabs(ct0[i]);
+      pht_l -= mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU);
+      tht = gsum<G>(tht_l, xw);
+      pht = gsum<G>(pht_l, xw);
+      const double inF = (k < nfilt && tht >= fth && pht >= fph) ? 1.0 : 0.0;
+      infilter = gmax<G>(inF, xw) > 0.5;
+    };
+    // acceptance of a trial point for step length al (W&B 2006 A-5.4): sufficient decrease
+    // (switching condition + Armijo, or theta/phi decrease), then the filter -- IPOPT's order,
+    // which decides whether a rejection was the filter's
+    auto acceptable = [&](double tht, double pht, bool infilter, double al, bool& ft) __attribute__((always_inline)) {
+      bool acc = isfinite(pht) && isfinite(tht) && tht <= theta_max;
+      ft = false;
+      if (acc) {
+        const bool sw = gd < 0 && al > sw_a;
+        if (thk <= theta_min && sw) {
+          acc = pht - phk <= kEtaPhi * al * gd + 10.0 * kEps * fabs(phk);
+          ft = acc;
+        } else {
+          acc = tht <= (1.0 - kGammaTheta) * thk || pht <= phk - kGammaPhi * thk + 10.0 * kEps * fabs(phk);
+        }
+      }
+      if (acc && infilter) {
+        acc = false;
+        lastrej_f = true;
+      } else if (!acc) {
+        lastrej_f = false;
+      }
+      return acc;
+    };
+    for (int ls = 0; ls < 80; ++ls) {
+      if (!__any(searching)) break;
+      double zt[NZ];
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) zt[i] = fma(alpha, dz[i], z[i]);  // the update's exact expression
+      double tht, pht;
+      bool infilter;
+      double ct[NX], ct0[NX];  // constraint values at the trial point (value path)
+      trial_value(zt, tht, pht, infilter, ct, ct0);
+      bool soc_want = false;  // first trial rejected with more infeasibility: second-order correction
+      if (searching) {
+        bool ft;
+        const bool acc = acceptable(tht, pht, infilter, alpha, ft);
+        if (infilter) DIAG(6);
+        if (acc) {
+          searching = false;
+          accepted = true;
+          ftype = ft;
+          if (ft) DIAG(7);
+        } else {
+          DIAG(2);
+          DIAG_IF(ls == 0 && tht >= thk, 10);
+          soc_want = ls == 0 && tht >= thk;
+          if (!soc_want) {
+            alpha *= 0.5;
+            if (alpha < amin) searching = false;  // would need restoration
+          }
+        }
+      }
+      {
+        // IPOPT's second-order correction (W&B 2006 A-5.7-A-5.9, max_soc = 4, kappa_soc = 0.99):
+        // re-solve the Newton system (same factorisation) with the constraint residual
+        // c_soc = alpha c(x_k) + c(x_trial), step to the boundary along the correction, and
+        // test it with the first trial's step length; accumulate and retry while the
+        // infeasibility keeps shrinking by kappa_soc
+        if (ls == 0 && __any(soc_want)) {
+          bool son = soc_want;
+          double cs[NX], cs0[NX];
+#pragma unroll
+          for (int i = 0; i < NX; ++i) {
+            cs[i] = fma(alpha, cdef[i], ct[i]);
+            cs0[i] = fma(alpha, c0[i], ct0[i]);
+          }
+          double th_old = thk;
+          double Pn1[NP];  // P_{k+1}
+          group_next<G, NP>(Pk, Pn1, xw);
+          for (int ps = 0; ps < 4; ++ps) {
+            if (!__any(son)) break;
+            // backward recursion of the value function's linear part only (the factorisation
+            // P_k, K_k, Huu' is the current iteration's): p_k = gx + K^T gu with
+            // s = p_{k+1} + P_{k+1} c_soc, gx = gp_x + A^T s, gu = gp_u + B^T s; k_f = -Huu'^-1 gu
+            double pv[NX], kfs[NU];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) pv[i] = (k == N) ? gp[i] : 0.0;
+#pragma unroll
+            for (int l = 0; l < NU; ++l) kfs[l] = 0.0;
+            auto soc_step = [&](const double* pin) __attribute__((always_inline)) {
+              const double* Aop = Model::jacA(ctx, A);
+              const double* Bop = Model::jacB(ctx, Bm);
+              double sv[NX], gu[NU];
+#pragma unroll
+              for (int i = 0; i < NX; ++i) {
+                double acc = pin[i];
+#pragma unroll
+                for (int m = 0; m < NX; ++m) acc = fma(Pn1[symix(i, m, NX)], cs[m], acc);
+                sv[i] = acc;
+              }
+#pragma unroll
+              for (int l = 0; l < NU; ++l) {
+                double acc = gp[NX + l];
+#pragma unroll
+                for (int m = 0; m < NX; ++m)
+                  if (Model::BMASK & (1ull << (m * NU + l))) acc = fma(Bop[m * NU + l], sv[m], acc);
+                gu[l] = acc;
+              }
+#pragma unroll
+              for (int i = 0; i < NX; ++i) {
+                double acc = gp[i];
+#pragma unroll
+                for (int m = 0; m < NX; ++m)
+                  if (Model::AMASK & (1ull << (m * NX + i))) acc = fma(Aop[m * NX + i], sv[m], acc);
+#pragma unroll
+                for (int l = 0; l < NU; ++l) acc = fma(Kk[l * NX + i], gu[l], acc);
+                pv[i] = acc;
+              }
+              if constexpr (NU == 1) {
+                kfs[0] = -fac.r0 * gu[0];
+              } else {
+                const double z1 = fac.r1 * fma(-fac.t, gu[0], gu[1]);
+                kfs[1] = -z1;
+                kfs[0] = -fma(fac.r0, gu[0], -fac.t * z1);
+              }
+            };
+            if constexpr (G <= 64) {
+              for (int j = N - 1; j >= 0; --j) {
+                double pin[NX];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) pin[i] = from_next(pv[i]);
+                if (k == j) soc_step(pin);
+              }
+            } else {  // wave by wave, N-side first; p crosses waves through LDS
+              const int wv = (int)(threadIdx.x >> 6);
+              for (int ph = XWave<G>::W - 1; ph >= 0; --ph) {
+                if (wv == ph) {
+                  const double* in = xw.prev();
+                  const int jtop = 64 * ph + 63;
+                  for (int j = min(N - 1, jtop); j >= 64 * ph; --j) {
+                    double pin[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) pin[i] = from_next(pv[i]);
+                    if (j == jtop && lane == 63)
+#pragma unroll
+                      for (int i = 0; i < NX; ++i) pin[i] = in[i];
+                    if (k == j) soc_step(pin);
+                  }
+                  if (ph > 0 && lane == 0) {
+                    double* out = xw.cur();
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) out[i] = pv[i];
+                  }
+                }
+                xw.sync();
+              }
+            }
+            double dzs[NZ], dls[NX];
+            forward(cs, kfs, pv, cs0, dzs, dls);
+            // primal and dual fraction to the boundary along the correction
+            double am_l = 1.0, azs_l = 1.0, dzLs[NZ], dzUs[NZ];
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) {
+              dzLs[i] = dzUs[i] = 0.0;
+              const double rdz = rcp64(dzs[i]);
+              if (hL[i]) {
+                const double sl = z[i] - lb[i], rs = rcp64(sl);
+                dzLs[i] = fma(mu, rs, -zL[i]) - zL[i] * rs * dzs[i];
+                if (dzs[i] < 0) am_l = fmin(am_l, -tau * sl * rdz);
+                if (dzLs[i] < 0) azs_l = fmin(azs_l, -tau * zL[i] * rcp64(dzLs[i]));
+              }
+              if (hU[i]) {
+                const double su = ub[i] - z[i], rs = rcp64(su);
+                dzUs[i] = fma(mu, rs, -zU[i]) + zU[i] * rs * dzs[i];
+                if (dzs[i] > 0) am_l = fmin(am_l, tau * su * rdz);
+                if (dzUs[i] < 0) azs_l = fmin(azs_l, -tau * zU[i] * rcp64(dzUs[i]));
+              }
+            }
+            const double as = gmin<G>(am_l, xw), azs = gmin<G>(azs_l, xw);
+            double zs[NZ];
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) zs[i] = fma(as, dzs[i], z[i]);
+            double ths, phs, cts[NX], cts0[NX];
+            bool infs;
+            trial_value(zs, ths, phs, infs, cts, cts0);
+#ifdef MPCX_DEBUG_PRINT
+            if (inst == 0 && k == 0)
+              printf("SOC it=%d ps=%d son=%d alpha0=%g as=%g thk=%.17g phk=%.17g ths=%.17g phs=%.17g infs=%d nfilt=%d\n", it,
+                     ps, (int)son, alpha, as, thk, phk, ths, phs, (int)infs, nfilt);
+#endif
+            if (son) {
+              bool ft;
+              if (acceptable(ths, phs, infs, alpha, ft)) {  // tested with the first trial's alpha
+                son = false;
+                searching = false;
+                accepted = true;
+                ftype = ft;
+                alpha = as;
+                az = azs;
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) {
+                  dz[i] = dzs[i];
+                  dzL[i] = dzLs[i];
+                  dzU[i] = dzUs[i];
+                }
+#pragma unroll
+                for (int i = 0; i < NX; ++i) dlam[i] = dls[i];
+                DIAG(11);
+              } else if (ps == 3 || ths > 0.99 * th_old) {
+                son = false;
+              } else {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                  cs[i] = fma(as, cs[i], cts[i]);
+                  cs0[i] = fma(as, cs0[i], cts0[i]);
+                }
+                th_old = ths;
+              }
+            }
+          }
+          if (soc_want && searching) {  // correction failed: backtrack along the original direction
+            alpha *= 0.5;
+            if (alpha < amin) searching = false;
+          }
+        }
+      }
+    }
     }
     if (!done && !accepted) {
       done = true;

@@ -22,7 +22,7 @@ from mpcx import dist as mdist  # noqa: E402
 from mpcx.device import DeviceLoop  # noqa: E402
 
 NAMES = ["regularised_iters", "extra_factorisations", "backtracks", "barrier_updates", "ftb_limited_steps",
-         "tiny_steps", "filter_rejections", "armijo_acceptances", "scan_fallbacks", "filter_resets"]
+         "tiny_steps", "filter_rejections", "armijo_acceptances", "scan_fallbacks", "filter_resets", "soc_eligible", "soc_accepted"]
 ND = len(NAMES)  # counters per instance (solver.hip kDiag)
 
 
@@ -53,12 +53,14 @@ def main():
         P0 = mdist.config5_swingup_inputs(0, B)
     solver = mpcx.nlpsol("s", "mi355x", ocp, {"ipopt": {"max_iter": 3000}})
     loop = DeviceLoop(solver, P0)
-    its, sts, cnt, Ps, W0 = [], [], [], [], []
+    its, sts, cnt, Ps, W0, L0, LX0 = [], [], [], [], [], [], []
     for s in range(S):
         if refs is not None:
             loop.set_stage_refs(torch.from_numpy(np.ascontiguousarray(refs[s])).cuda())
         Ps.append(loop.P.cpu().numpy().copy())
         W0.append(loop.w0.cpu().numpy().copy())
+        L0.append(loop.lam0.cpu().numpy().copy())
+        LX0.append(loop.lamx0.cpu().numpy().copy())
         loop.step()
         torch.cuda.synchronize()
         its.append(loop.iters.cpu().numpy().copy())
@@ -78,6 +80,7 @@ def main():
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     np.savez(os.path.join(ROOT, "gpurun_out", f"ode_diag_{model}.npz"),
              P=np.array([Ps[w // B][w % B] for w in worst]), w0=np.array([W0[w // B][w % B] for w in worst]),
+             lam0=np.array([L0[w // B][w % B] for w in worst]), lamx0=np.array([LX0[w // B][w % B] for w in worst]),
              step=worst // B, inst=worst % B, iters=fi[worst], status=sts.ravel()[worst])
 
 
