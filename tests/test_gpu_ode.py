@@ -167,3 +167,27 @@ def test_ode_run_equals_lockstep(mpcx, which, N):
     assert np.all(np.array(st_l) == 0)
     for n in ("P", "w", "w0", "lam", "lamx", "f"):
         np.testing.assert_array_equal(getattr(run, n).cpu().numpy(), getattr(lock, n).cpu().numpy(), err_msg=n)
+
+
+def test_dyn_bicycle_hardest_instances_are_kkt_points(mpcx):
+    """Config-4 variant (6-state bicycle, bench inputs), first closed-loop step from the cold start:
+    the instances that needed the most iterations -- the ones the second-order correction acts on
+    (solver.hip, Dyn::kSOC) -- end at points the oracle certifies as KKT points of the NLP, and the
+    iteration tail stays short (before the correction the worst cold solve took 308 iterations)."""
+    from mpcx import dist as mdist
+    from oracle import ode_ref
+
+    B, N = 256, 50
+    ocp = mpcx.dynamic_bicycle_lane_change(N=N)
+    t0, x0, (X, Y, V) = mdist.config4_bicycle_inputs(0, B)
+    refs = np.stack([mpcx.ode.dyn_bicycle_references(X, Y, V, int(t), N).reshape(-1) for t in t0])
+    P = ocp.params(x0, refs)
+    solver = mpcx.nlpsol("dyn", "mi355x", ocp, {"ipopt": {"max_iter": 3000}})
+    r = solver.solve_batch(P)
+    assert np.mean(r["status"] == 0) >= 0.99, np.unique(r["status"], return_counts=True)
+    assert r["iters"].max() < 250, r["iters"].max()
+    pr = ode_ref.Problem(ocp)
+    hard = [b for b in np.argsort(-r["iters"]) if r["status"][b] == 0][:6]
+    for b in hard:
+        kkt, gres = pr.kkt_residual(r["w"][b], r["lam_g"][b], r["lam_x"][b], P[b])
+        assert kkt <= 1e-6 and gres <= 1e-9, (b, int(r["iters"][b]), kkt, gres)
