@@ -84,7 +84,8 @@ def test_ode_plant_matches_oracle(mpcx, which):
 
 @pytest.mark.parametrize("policy", [0, 1])
 @pytest.mark.parametrize("which,N,B", [("kin_bicycle", 30, 6), ("dyn_bicycle", 20, 4), ("cartpole", 50, 6),
-                                       ("kin_bicycle", 1, 5), ("cartpole", 15, 5), ("cartpole", 130, 3)])
+                                       ("kin_bicycle", 1, 5), ("cartpole", 15, 5), ("cartpole", 130, 3),
+                                       ("dyn_bicycle", 70, 3)])
 def test_ode_optimum_matches_oracle(mpcx, which, N, B, policy):
     from oracle import ode_ref
 
@@ -96,6 +97,13 @@ def test_ode_optimum_matches_oracle(mpcx, which, N, B, policy):
     assert np.all(r["status"] == 0), r["status"]
     pr = ode_ref.Problem(ocp)
     for b in range(B):
+        if which == "dyn_bicycle" and N > 50:
+            # two-wave group (sequential multi-wave Riccati, NX = 6): the oracle's single-shooting
+            # Newton is ill-conditioned over 70 intervals of this model, so the point is certified
+            # by the multiple-shooting KKT residual alone
+            kkt, gres = pr.kkt_residual(r["w"][b], r["lam_g"][b], r["lam_x"][b], P[b])
+            assert kkt <= 1e-6 and gres <= 1e-9, (b, kkt, gres)
+            continue
         X, U = pr.split_w(r["w"][b])
         Uo, Xo, info = pr.solve(P[b], U0=U)  # started at the GPU point: same local optimum
         assert info["status"] in ("converged", "stalled") and info["pg"] <= 1e-6, info
@@ -104,7 +112,7 @@ def test_ode_optimum_matches_oracle(mpcx, which, N, B, policy):
         assert abs(r["f"][b] - info["J"]) <= 1e-8 * max(1.0, abs(info["J"]))
         kkt, gres = pr.kkt_residual(r["w"][b], r["lam_g"][b], r["lam_x"][b], P[b])
         assert kkt <= 1e-6 and gres <= 1e-9, (b, kkt, gres)
-    if which == "dyn_bicycle":  # the vx >= 2.5 bound stays inactive (the oracle does not model it)
+    if which == "dyn_bicycle" and N <= 50:  # the vx >= 2.5 bound stays inactive (the oracle's solve does not model it)
         assert np.min(r["w"][:, 3::8]) > 2.6
 
 
