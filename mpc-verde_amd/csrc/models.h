@@ -14,6 +14,9 @@
 #ifndef MPCX_PSCAN_DEFAULT
 #define MPCX_PSCAN_DEFAULT true
 #endif
+#ifndef MPCX_SCAN_MAX_NX
+#define MPCX_SCAN_MAX_NX 4
+#endif
 #ifndef MPCX_PSCAN_UNICYCLE
 #define MPCX_PSCAN_UNICYCLE false
 #endif
@@ -90,7 +93,7 @@ struct LinearModel {
   // scan with register tables, 12.6 M scan with table operands; config 5 (NX = 5, N = 100)
   // 0.91 M sequential, 0.43 M / 0.87 M with the scan (its 65-double elements still spill), so
   // NX = 5 keeps the sequential recursion and register tables.
-  static constexpr bool kScan = MPCX_PSCAN_DEFAULT && NX_ <= 4;
+  static constexpr bool kScan = MPCX_PSCAN_DEFAULT && NX_ <= MPCX_SCAN_MAX_NX;
   static constexpr bool kParallelRiccati = kScan, kTableJac = kScan, kTableHess = kScan;
   __device__ __forceinline__ static const double* jacA(const Ctx& c, const double* A) { return kTableJac ? c.A : A; }
   __device__ __forceinline__ static const double* jacB(const Ctx& c, const double* B) { return kTableJac ? c.B : B; }
