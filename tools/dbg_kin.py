@@ -1,3 +1,8 @@
+"""Replays one saved kinematic-bicycle solve (gpurun_out/ode_diag_kin_bicycle.npz, written by
+tools/ode_diag.py: parameters, primal and dual warm start of the slowest instances) on the
+debug build, which prints the optimality error and the second-order-correction trials of
+instance 0 per iteration (make -C mpc-verde_amd debug; python tools/dbg_kin.py [max_iter]).
+"""
 import os, sys
 import numpy as np
 ROOT = os.environ.get("GRAFT_REPO_ROOT", "/root/repo")
