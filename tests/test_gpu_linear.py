@@ -303,3 +303,37 @@ def test_random_linear_problems_vs_lq_oracle(mpcx, R, nx, seed):
             n_active += int(np.any(np.abs(U_ref) >= 1 - 1e-9))
         if N > 1:
             assert n_active >= B // 4  # the bounds matter
+
+
+def test_scan_fallback_on_indefinite_stage_weights(mpcx, R):
+    """Stage control weight slightly negative (W_uu = -0.05) under a large state weight: the stage
+    R = Hd_uu is indefinite wherever the barrier terms do not cover it, so the log-depth Riccati
+    scan (pscan.h) cannot build its elements and the instance takes the sequential recursion
+    instead, while the reduced Huu' = R + B^T P B stays positive definite (the condensed QP is
+    convex).  The optimum must still match the LQ oracle.  (With the negative weight on the
+    last stage too, whose x_N carries no cost, the QP is concave in u_{N-1}: the GPU then lands
+    on the bound -- a minimiser -- where the oracle's active-set method stops at u = 0.)"""
+    from mpcx import lti
+
+    rng = np.random.default_rng(11)
+    nx, nu, N, B = 4, 1, 20, 32
+    A = np.eye(nx) + 0.05 * rng.normal(size=(nx, nx))
+    Bm = rng.normal(size=(nx, nu)) + 1.0
+    W = np.zeros((2, nx + nu, nx + nu))
+    W[:, :nx, :nx] = 5.0 * np.eye(nx)
+    W[0, nx, nx] = -0.05  # stages 0..N-2: indefinite stage R, convex through P_{k+1}
+    W[1, nx, nx] = 0.5    # last stage: x_N carries no cost, so its control needs its own weight
+    tab = np.zeros(N, np.int32)
+    tab[-1] = 1
+    lin = lti.LinearOCP(N=N, A=np.stack([A, A]), B=np.stack([Bm, Bm]), c=np.zeros((2, nx)), W=W, tab=tab,
+                        u_lb=(-1.0,), u_ub=(1.0,))
+    S = mpcx.nlpsol("fb", "mi355x", lin, {"ipopt": {"max_iter": 300}})
+    x0 = rng.normal(size=(B, nx))
+    zr = np.zeros((B, N, nx + nu))
+    r = S.solve_batch(lin.params(x0, zr))
+    assert np.all(r["status"] == 0), np.unique(r["status"], return_counts=True)
+    U = U_of(r["w"], nx, nu, N)[..., 0]
+    for b in range(B):
+        _, U_ref, J = R.lq_solve(x0[b], lin.A, lin.B, lin.c, lin.W, lin.tab, zr[b], [-1.0], [1.0])
+        assert rel(U[b], U_ref[:, 0]) <= 1e-5, b
+        assert abs(r["f"][b] - J) <= 1e-7 * max(1.0, abs(J)), b
