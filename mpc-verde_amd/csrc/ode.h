@@ -18,9 +18,13 @@
 // Derivatives.  A hyper-dual number v + a e1 + b e2 + ab e1e2 (e1^2 = e2^2 = 0) carries the
 // first derivatives along two seed directions and the mixed second derivative.  One RK4 pass
 // seeded with (e_i, e_j) gives columns i and j of dF/dz and d2F/dz_i dz_j exactly (no
-// truncation).  Passes run over the pairs of variables that enter f nonlinearly (NLMASK) plus
-// one pass per remaining variable; the passes share one RK4 body (runtime loop) so code size
-// does not grow with the pair count.  The stage cost is the mpctools node cost
+// truncation).  Passes run over the pairs of variables whose second derivatives through the RK4
+// map can be non-zero (NLMASK) plus one pass per remaining variable; the passes share one RK4
+// body (runtime loop) so code size does not grow with the pair count.  NLMASK is every variable
+// f reads, not only those entering f nonlinearly: RK4 composes f with itself, so a variable
+// that enters f linearly (the bicycle's ax) still couples nonlinearly through the states it
+// drives (d2F/dax dvx != 0; tests/test_ode_cpu.py checks the mask against the oracle's
+// Hessian).  Variables f never reads (INDEP) have unit Jacobian columns and no curvature.  The stage cost is the mpctools node cost
 // l = sum Q_i (x_i - xr_i)^2 + sum R_j (u_j - ur_j)^2 (exact gradient and Hessian in closed form).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -88,8 +92,9 @@ struct KinBicycle {
 struct DynBicycle {
   static constexpr int NX = 6, NU = 2;
   static constexpr bool kSOC = true;
-  // psi, vx, vy, r, delta (ax enters linearly, X and Y not at all)
-  static constexpr unsigned NLMASK = (1u << 2) | (1u << 3) | (1u << 4) | (1u << 5) | (1u << 6);
+  // psi, vx, vy, r, delta and ax: ax enters f linearly but drives vx, which enters nonlinearly,
+  // so F has d2F/dax dz != 0 (X and Y are not read at all)
+  static constexpr unsigned NLMASK = (1u << 2) | (1u << 3) | (1u << 4) | (1u << 5) | (1u << 6) | (1u << 7);
   static constexpr unsigned INDEP = (1u << 0) | (1u << 1);
   template <class S>
   __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx) {

@@ -119,3 +119,55 @@ def test_oracle_single_shooting_optimum_is_ms_kkt_point(which):
         lam_x[nx + nz * k: nx + nz * k + nu] = -g.reshape(N, nu)[k]
     r, gres = pr.kkt_residual(pr.join_w(X, U), lam.reshape(-1), lam_x, P)
     assert r < 1e-9 and gres < 1e-12
+
+
+def _kernel_masks():
+    """NLMASK / INDEP of each ODE model as written in mpc-verde_amd/csrc/ode.h."""
+    import re
+
+    src = open(os.path.join(ROOT, "mpc-verde_amd", "csrc", "ode.h")).read()
+    out = {}
+    for name, model in (("KinBicycle", "kin_bicycle"), ("DynBicycle", "dyn_bicycle"), ("CartPole", "cartpole")):
+        body = src[src.index(f"struct {name} {{"):]
+        body = body[:body.index("};")]
+        bits = {}
+        for key in ("NLMASK", "INDEP"):
+            expr = re.search(rf"{key} = ([^;]*);", body).group(1)
+            bits[key] = {int(b) for b in re.findall(r"1u << (\d+)", expr)}
+        out[model] = bits
+    return out
+
+
+@pytest.mark.parametrize("model", ["kin_bicycle", "dyn_bicycle", "cartpole"])
+def test_kernel_hessian_passes_cover_the_curvature(model):
+    """The kernel's exact Hessian of lam^T F (ode.h OdeModel::derivs) runs hyper-dual passes over
+    the pairs of NLMASK variables and one diagonal pass per other variable f reads; it takes every
+    other entry of d2(lam^T F)/dz2 as zero and the INDEP variables' Jacobian columns as unit
+    vectors.  Check both against the oracle (complex-step Jacobians, central differences) at
+    random points: a variable that enters f linearly but drives a state that enters nonlinearly
+    (the bicycle's ax -> vx) must be in NLMASK, since RK4 composes f with itself."""
+    from mpcx import ode
+    from oracle import ode_ref
+
+    masks = _kernel_masks()[model]
+    ocp = {"kin_bicycle": ode.kinematic_bicycle_tracking, "dyn_bicycle": ode.dynamic_bicycle_lane_change,
+           "cartpole": ode.cartpole_swingup}[model](N=5)
+    pr = ode_ref.Problem(ocp)
+    nx, nz = pr.nx, pr.nz
+    rng = np.random.default_rng(3)
+    for _ in range(4):
+        z = rng.uniform(-0.5, 0.5, nz)
+        if model == "dyn_bicycle":
+            z[3] = rng.uniform(3.0, 8.0)  # vx away from 0 (1/vx)
+        lam = rng.normal(size=nx)
+        H = pr.hess_lam(z, lam)
+        J = pr.jac(z)
+        scale = max(1.0, np.abs(H).max())
+        for i in range(nz):
+            for j in range(i, nz):
+                covered = (i in masks["NLMASK"] and j in masks["NLMASK"]) or (i == j and i not in masks["INDEP"])
+                if not covered:
+                    assert abs(H[i, j]) <= 1e-6 * scale, (model, i, j, H[i, j])
+        for j in masks["INDEP"]:
+            np.testing.assert_allclose(J[:, j], np.eye(nx)[:, j], atol=1e-12)
+            assert np.abs(H[j]).max() <= 1e-6 * scale
