@@ -44,6 +44,7 @@ struct UnicycleModel {
   };
   // Jacobian/Hessian operands of the Newton step live in the kernel's registers
   static constexpr bool kTableJac = false, kTableHess = false;
+  static constexpr int kTrigSlots = 0;  // no LDS value cache
   __device__ __forceinline__ static const double* jacA(const Ctx&, const double* A) { return A; }
   __device__ __forceinline__ static const double* jacB(const Ctx&, const double* B) { return B; }
   __device__ __forceinline__ static const double* hessW(const Ctx&, const double* H) { return H; }
@@ -95,6 +96,7 @@ struct LinearModel {
   // NX = 5 keeps the sequential recursion and register tables.
   static constexpr bool kScan = MPCX_PSCAN_DEFAULT && NX_ <= MPCX_SCAN_MAX_NX;
   static constexpr bool kParallelRiccati = kScan, kTableJac = kScan, kTableHess = kScan;
+  static constexpr int kTrigSlots = 0;
   __device__ __forceinline__ static const double* jacA(const Ctx& c, const double* A) { return kTableJac ? c.A : A; }
   __device__ __forceinline__ static const double* jacB(const Ctx& c, const double* B) { return kTableJac ? c.B : B; }
   __device__ __forceinline__ static const double* hessW(const Ctx& c, const double* H) { return kTableHess ? c.W : H; }

@@ -75,17 +75,93 @@ __device__ __forceinline__ HD tan(HD x) {
   return {t, d * x.a, d * x.b, fma(d, x.ab, 2.0 * t * d * x.a * x.b)};
 }
 
+// Transcendental values of f's stage evaluations.  Every hyper-dual pass runs RK4 through
+// the same stage points (the passes differ only in their seed directions), so the value parts
+// of sin/cos/tan/reciprocals are the same in every pass: the value pass records them in a
+// per-lane LDS cache (TrigRecord), the passes read them back (TrigReplay) and only form the
+// derivative parts.  TrigDirect evaluates (value(), plants, horizons past the cache).
+// Arguments tagged _u depend on the inputs only (constant over the RK4 substeps): one slot.
+struct TrigDirect {
+  __device__ __forceinline__ void sincos_x(double x, double& s, double& c) { ::sincos(x, &s, &c); }
+  __device__ __forceinline__ void sincos_u(double x, double& s, double& c) { ::sincos(x, &s, &c); }
+  __device__ __forceinline__ double recip_x(double x) { return 1.0 / x; }
+  __device__ __forceinline__ double div_x(double n, double d) { return n / d; }
+  __device__ __forceinline__ double tan_u(double x) { return ::tan(x); }
+  __device__ __forceinline__ void sincos_x(HD x, HD& s, HD& c) { s = sin(x); c = cos(x); }
+  __device__ __forceinline__ void sincos_u(HD x, HD& s, HD& c) { s = sin(x); c = cos(x); }
+  __device__ __forceinline__ HD recip_x(HD x) { return recip(x); }
+  __device__ __forceinline__ HD div_x(HD n, HD d) { return n / d; }
+  __device__ __forceinline__ HD tan_u(HD x) { return tan(x); }
+};
+// slots: [0, 2) input-only (sincos_u or tan_u), then per stage evaluation in call order
+struct TrigRecord {
+  double* buf;  // this lane's slot 0; slot i at buf[i * stride]
+  int stride, idx;
+  __device__ __forceinline__ void put(double v) { buf[(idx++) * stride] = v; }
+  __device__ __forceinline__ void sincos_x(double x, double& s, double& c) {
+    ::sincos(x, &s, &c);
+    put(s);
+    put(c);
+  }
+  __device__ __forceinline__ void sincos_u(double x, double& s, double& c) {
+    ::sincos(x, &s, &c);
+    buf[0] = s;
+    buf[stride] = c;
+  }
+  __device__ __forceinline__ double recip_x(double x) {
+    const double r = 1.0 / x;
+    put(r);
+    return r;
+  }
+  // n / d as an IEEE division (the value path keeps its bits); 1/d recorded for the passes
+  __device__ __forceinline__ double div_x(double n, double d) {
+    put(1.0 / d);
+    return n / d;
+  }
+  __device__ __forceinline__ double tan_u(double x) {
+    const double t = ::tan(x);
+    buf[0] = t;
+    return t;
+  }
+};
+struct TrigReplay {
+  const double* buf;
+  int stride, idx;
+  __device__ __forceinline__ double get() { return buf[(idx++) * stride]; }
+  __device__ __forceinline__ static void sc(double sv, double cv, HD x, HD& s, HD& c) {
+    s = {sv, cv * x.a, cv * x.b, fma(cv, x.ab, -sv * x.a * x.b)};
+    c = {cv, -sv * x.a, -sv * x.b, -fma(sv, x.ab, cv * x.a * x.b)};
+  }
+  __device__ __forceinline__ void sincos_x(HD x, HD& s, HD& c) {
+    const double sv = get(), cv = get();
+    sc(sv, cv, x, s, c);
+  }
+  __device__ __forceinline__ void sincos_u(HD x, HD& s, HD& c) { sc(buf[0], buf[stride], x, s, c); }
+  __device__ __forceinline__ HD recip_x(HD y) {
+    const double r = get(), m = -r * r;
+    return {r, m * y.a, m * y.b, fma(m, y.ab, -2.0 * m * r * y.a * y.b)};
+  }
+  __device__ __forceinline__ HD div_x(HD n, HD d) { return n * recip_x(d); }
+  __device__ __forceinline__ HD tan_u(HD x) {
+    const double t = buf[0], d = fma(t, t, 1.0);
+    return {t, d * x.a, d * x.b, fma(d, x.ab, 2.0 * t * d * x.a * x.b)};
+  }
+};
+
 // ---------------------------------------------------------------------------- dynamics
 struct KinBicycle {
   static constexpr int NX = 3, NU = 2;
   static constexpr bool kSOC = false;
   static constexpr unsigned NLMASK = (1u << 2) | (1u << 3) | (1u << 4);  // psi, v, delta
   static constexpr unsigned INDEP = (1u << 0) | (1u << 1);               // f does not read X, Y
-  template <class S>
-  __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx) {
-    dx[0] = u[0] * cos(x[2]);
-    dx[1] = u[0] * sin(x[2]);
-    dx[2] = u[0] * tan(u[1]) * (1.0 / par[0]);  // par = (L)
+  static constexpr int kTrigPerEval = 2, kTrigInput = 1, kTrigMaxM = 1;  // sincos(psi); tan(delta)
+  template <class S, class Tc>
+  __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx, Tc& tc) {
+    S sp, cp;
+    tc.sincos_x(x[2], sp, cp);
+    dx[0] = u[0] * cp;
+    dx[1] = u[0] * sp;
+    dx[2] = u[0] * tc.tan_u(u[1]) * (1.0 / par[0]);  // par = (L)
   }
 };
 
@@ -96,15 +172,18 @@ struct DynBicycle {
   // so F has d2F/dax dz != 0 (X and Y are not read at all)
   static constexpr unsigned NLMASK = (1u << 2) | (1u << 3) | (1u << 4) | (1u << 5) | (1u << 6) | (1u << 7);
   static constexpr unsigned INDEP = (1u << 0) | (1u << 1);
-  template <class S>
-  __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx) {
+  static constexpr int kTrigPerEval = 3, kTrigInput = 2, kTrigMaxM = 4;  // sincos(psi), 1/vx; sincos(delta)
+  template <class S, class Tc>
+  __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx, Tc& tc) {
     // par = (m, a, b, Ca, Jz): Trajectory_tracking_dynamic_model.py:36-40 (a, b = CG-axle distances)
     const double m = par[0], a = par[1], b = par[2], Ca2 = 2.0 * par[3], Jz = par[4];
     const S psi = x[2], vx = x[3], vy = x[4], r = x[5], d = u[0];
-    const S ivx = 1.0 / vx;
+    S sp, cp, sd, cd;
+    tc.sincos_x(psi, sp, cp);
+    const S ivx = tc.recip_x(vx);
+    tc.sincos_u(d, sd, cd);
     const S Fyf = Ca2 * (d - (vy + a * r) * ivx);  // front axle: slip angle delta - (vy + a r)/vx
     const S Fyr = -Ca2 * ((vy - b * r) * ivx);     // rear axle: -(vy - b r)/vx
-    const S sp = sin(psi), cp = cos(psi), sd = sin(d), cd = cos(d);
     dx[0] = vx * cp - vy * sp;
     dx[1] = vx * sp + vy * cp;
     dx[2] = r;
@@ -119,12 +198,14 @@ struct CartPole {
   static constexpr bool kSOC = false;
   static constexpr unsigned NLMASK = (1u << 1) | (1u << 2) | (1u << 3) | (1u << 4);  // p', phi, phi', F
   static constexpr unsigned INDEP = (1u << 0);                                        // f does not read p
-  template <class S>
-  __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx) {
+  static constexpr int kTrigPerEval = 3, kTrigInput = 0, kTrigMaxM = 1;  // sincos(phi), 1/(M + m sin^2 phi)
+  template <class S, class Tc>
+  __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx, Tc& tc) {
     // par = (M, m, L, g, c); phi measured so that the upright linearisation is the reference's Ac
     const double Mc = par[0], m = par[1], L = par[2], g = par[3], c = par[4];
-    const S s = sin(x[2]), co = cos(x[2]);
-    const S pdd = (u[0] - c * x[1] - (m * L) * (x[3] * x[3]) * s + (m * g) * (s * co)) / (Mc + m * (s * s));
+    S s, co;
+    tc.sincos_x(x[2], s, co);
+    const S pdd = tc.div_x(u[0] - c * x[1] - (m * L) * (x[3] * x[3]) * s + (m * g) * (s * co), Mc + m * (s * s));
     dx[0] = x[1];
     dx[1] = pdd;
     dx[2] = x[3];
@@ -133,8 +214,8 @@ struct CartPole {
 };
 
 // RK4, M substeps, one f call site (the four stages are a runtime loop)
-template <class Dyn, class S>
-__device__ __forceinline__ void ode_rk4(const S* x0, const S* u, const OdeParams& op, S* xf) {
+template <class Dyn, class S, class Tc>
+__device__ __forceinline__ void ode_rk4(const S* x0, const S* u, const OdeParams& op, S* xf, Tc& tc) {
   constexpr int NX = Dyn::NX;
   S x[NX];
 #pragma unroll
@@ -147,7 +228,7 @@ __device__ __forceinline__ void ode_rk4(const S* x0, const S* u, const OdeParams
     for (int i = 0; i < NX; ++i) xt[i] = x[i];
 #pragma unroll 1
     for (int st = 0; st < 4; ++st) {
-      Dyn::f(xt, u, op.par, k);
+      Dyn::f(xt, u, op.par, k, tc);
       const double wa = (st == 0 || st == 3) ? 1.0 : 2.0;  // k1 + 2 k2 + 2 k3 + k4
       const double cn = (st == 2) ? h : 0.5 * h;           // next stage point x + c k
 #pragma unroll
@@ -205,8 +286,26 @@ struct OdeModel {
     }
   }
   __device__ __forceinline__ static double wgt(const ModelArgs& a, int i) { return i < NX ? a.op.Q[i] : a.op.R[i - NX]; }
+  // per-lane LDS cache of the stage evaluations' transcendental values (TrigRecord/Replay),
+  // for up to Dyn::kTrigMaxM RK4 substeps (each model's default M; a larger M evaluates
+  // directly) -- sized so that the cache and the Riccati scan buffer fit the LDS together
+  static constexpr int kTrigMaxM = Dyn::kTrigMaxM;
+  static constexpr int kTrigSlots = Dyn::kTrigInput + Dyn::kTrigPerEval * 4 * kTrigMaxM;
+  template <class Tc>
+  __device__ __forceinline__ static void value_tc(const ModelArgs& a, const Ctx& c, const double* z, double* xf,
+                                                  double& q, Tc& tc) {
+    ode_rk4<Dyn, double>(z, z + NX, a.op, xf, tc);
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+      const double d = z[i] - c.zr[i];
+      acc = fma(wgt(a, i) * d, d, acc);
+    }
+    q = acc;
+  }
   __device__ __forceinline__ static void value(const ModelArgs& a, const Ctx& c, const double* z, double* xf, double& q) {
-    ode_rk4<Dyn, double>(z, z + NX, a.op, xf);
+    TrigDirect tc;
+    ode_rk4<Dyn, double>(z, z + NX, a.op, xf, tc);
     double acc = 0.0;
 #pragma unroll
     for (int i = 0; i < NZ; ++i) {
@@ -217,7 +316,13 @@ struct OdeModel {
   }
   __device__ __forceinline__ static void derivs(const ModelArgs& a, const Ctx& c, const double* z, const double* ln, double fs,
                                                 double* xf, double& q, double* A, double* Bm, double* g, double* H) {
-    value(a, c, z, xf, q);
+    const bool cached = a.tc != nullptr && a.op.M <= kTrigMaxM;  // kernel-uniform
+    if (cached) {
+      TrigRecord rec{a.tc, a.tc_stride, Dyn::kTrigInput};
+      value_tc(a, c, z, xf, q, rec);
+    } else {
+      value(a, c, z, xf, q);
+    }
 #pragma unroll
     for (int i = 0; i < NH; ++i) H[i] = 0.0;
 #pragma unroll
@@ -248,7 +353,13 @@ struct OdeModel {
         HD zs[NZ], xs[NX];
 #pragma unroll
         for (int i = 0; i < NZ; ++i) zs[i] = HD{z[i], i == m ? 1.0 : 0.0, i == n ? 1.0 : 0.0, 0.0};
-        ode_rk4<Dyn, HD>(zs, zs + NX, a.op, xs);
+        if (cached) {
+          TrigReplay rp{a.tc, a.tc_stride, Dyn::kTrigInput};
+          ode_rk4<Dyn, HD>(zs, zs + NX, a.op, xs, rp);
+        } else {
+          TrigDirect td;
+          ode_rk4<Dyn, HD>(zs, zs + NX, a.op, xs, td);
+        }
         double s = 0.0;
 #pragma unroll
         for (int r = 0; r < NX; ++r) {

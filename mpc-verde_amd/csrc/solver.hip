@@ -123,6 +123,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   // LDS buffer of the Riccati scan (pscan.h): one element per thread, structure of arrays
   constexpr int kSBS = G > 64 ? G : 64;  // threads per block = field stride
   __shared__ double sbuf[Model::kParallelRiccati ? RElem<NX>::NE * kSBS : 1];
+  // LDS cache of the ODE models' transcendental values across their derivative passes (ode.h)
+  __shared__ double tcache[Model::kTrigSlots > 0 ? Model::kTrigSlots * kSBS : 1];
   XWave<G> xw{xch, 0};
   const int inst = (int)(gid / G);
   const bool valid = inst < a.B;
@@ -139,7 +141,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   if (valid)
 #pragma unroll
     for (int i = 0; i < NX; ++i) x0[i] = Pin[i];
-  const ModelArgs ma = model_args(a);
+  const ModelArgs ma = [&] {
+    ModelArgs m = model_args(a);
+    if (Model::kTrigSlots > 0) {
+      m.tc = tcache + threadIdx.x;
+      m.tc_stride = kSBS;
+    }
+    return m;
+  }();
   typename Model::Ctx ctx;
   Model::load_ctx(ma, valid ? inst : 0, Pin, k, hasU, ctx);
 
