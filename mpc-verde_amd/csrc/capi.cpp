@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -35,6 +36,7 @@ struct mpcx_handle {
   double *d_linA = nullptr, *d_linB = nullptr, *d_linc = nullptr, *d_linW = nullptr;
   int32_t* d_lintab = nullptr;
   int lin_ntab = 0, lin_rows = 0;
+  unsigned long long lin_dec = 0;  // LinTables::dec_mask
   const int32_t* ext_tab = nullptr;  // caller-owned device schedule (mpcx_set_linear_tab_dev)
   int ext_rows = 0;
   int n_simd = 0;  // SIMDs of the device (CUs x 4): the solve launch widens lane groups to fill them
@@ -394,6 +396,17 @@ int mpcx_set_linear_model(mpcx_handle* h, int32_t n_tab, const double* A, const 
   }
   h->lin_ntab = n_tab;
   h->lin_rows = tab_rows;
+  h->lin_dec = 0;
+  for (int j = 0; j < n_tab && j < 64; ++j) {
+    bool d = true;
+    for (int i = 0; i < nx * nu; ++i) d = d && B[(size_t)j * nx * nu + i] == 0.0;
+    for (int r = 0; r < nx; ++r)
+      for (int l = 0; l < nu; ++l) d = d && W[(size_t)j * nh + r * nz - r * (r - 1) / 2 + (nx + l - r)] == 0.0;
+    if (d) h->lin_dec |= 1ull << j;
+  }
+  // diagnostic knob: MPCX_DEC_SUFFIX=0 disables the reuse (tests compare both paths' bits)
+  if (const char* e = getenv("MPCX_DEC_SUFFIX"))
+    if (atoi(e) == 0) h->lin_dec = 0;
   return 0;
 }
 
@@ -432,6 +445,7 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
   a.lin.tab = h->ext_tab ? h->ext_tab : h->d_lintab;
   a.lin.per_instance = (h->ext_tab ? h->ext_rows : h->lin_rows) > 1 ? 1 : 0;
   a.lin.n_tab = h->lin_ntab;
+  a.lin.dec_mask = h->lin_dec;
   a.N = h->spec.N;
   a.max_iter = h->spec.max_iter;
   a.p_layout = h->spec.param_layout;

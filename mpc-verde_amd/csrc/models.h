@@ -86,6 +86,7 @@ struct LinearModel {
   struct Ctx {
     const double *A, *B, *c, *W;
     double zr[NZ];
+    bool dec;  // my stage's table is decoupled (LinTables::dec_mask)
   };
   // Log-depth Riccati scan (pscan.h), and with it A, B and the stage Hessian 2 W read from the
   // stage tables (global memory, cache-resident) instead of register copies held through the
@@ -96,6 +97,10 @@ struct LinearModel {
   // NX = 5 keeps the sequential recursion and register tables.
   static constexpr bool kScan = MPCX_PSCAN_DEFAULT && NX_ <= MPCX_SCAN_MAX_NX;
   static constexpr bool kParallelRiccati = kScan, kTableJac = kScan, kTableHess = kScan;
+  // Decoupled suffix (solver.hip): the sequential recursion reuses P_k on a suffix of
+  // decoupled stages -- the move-blocked stages of the cart-pole QP (lti.py).  Scan models
+  // keep their scan.
+  static constexpr bool kDecSuffix = !kScan;
   static constexpr int kTrigSlots = 0;
   __device__ __forceinline__ static const double* jacA(const Ctx& c, const double* A) { return kTableJac ? c.A : A; }
   __device__ __forceinline__ static const double* jacB(const Ctx& c, const double* B) { return kTableJac ? c.B : B; }
@@ -108,6 +113,7 @@ struct LinearModel {
     c.B = a.lin.B + (size_t)j * NX * NU;
     c.c = a.lin.c + (size_t)j * NX;
     c.W = a.lin.W + (size_t)j * NH;
+    c.dec = hasU && j < 64 && ((a.lin.dec_mask >> j) & 1ull);
     for (int i = 0; i < NZ; ++i) c.zr[i] = hasU ? P[NX + NZ * k + i] : 0.0;
   }
   __device__ __forceinline__ static void value(const ModelArgs& a, const Ctx& c, const double* z, double* xf, double& q) {

@@ -20,6 +20,15 @@ __host__ __device__ constexpr int symix(int i, int j, int n) {
   return i <= j ? i * n - i * (i - 1) / 2 + (j - i) : j * n - j * (j - 1) / 2 + (i - j);
 }
 
+// row i of P c for a packed symmetric P (the SREORD / DEC order)
+template <int NX>
+__device__ __forceinline__ double riccati_pc_row(const double* P, const double* c, int i) {
+  double acc = P[symix(i, 0, NX)] * c[0];
+#pragma unroll
+  for (int m = 1; m < NX; ++m) acc = fma(P[symix(i, m, NX)], c[m], acc);
+  return acc;
+}
+
 template <int NX, int NU>
 struct Fac {  // LDL^T data of Huu' kept for the gains (per lane)
   double r0, r1, t;  // 1/d0, 1/d1, L[1][0]
@@ -27,13 +36,35 @@ struct Fac {  // LDL^T data of Huu' kept for the gains (per lane)
   double g0, g1;          // L^{-1} gu'
 };
 
-template <int NX, int NU, unsigned long long AMASK, unsigned long long BMASK>
+//
+// DEC: the stage is decoupled -- its B is zero and its stage Hessian has no x-u block -- and
+// Pown holds the P_k this same step produced at the previous factorisation from identical
+// operands (same stage Hessian, A and P_{k+1}; the caller guarantees it, solver.hip
+// "decoupled suffix").  Then Hux' = 0, Huu' = Huu and P_k = Hxx + A^T P_{k+1} A is Pown
+// itself: the step only carries the vector part, p_k = gx + A^T (p_{k+1} + P_{k+1} c),
+// computed with the full step's operation order (same bits up to the sign of an exact zero).
+// SREORD: s = (P_{k+1} c) + p_{k+1} with the product summed first -- the order in which the
+// DEC step takes it precomputed off the chain (vpre = P_{k+1} c, riccati_pc), so the two
+// variants of a model that uses DEC give the same bits.
+template <int NX, int NU, unsigned long long AMASK, unsigned long long BMASK, bool DEC = false, bool SREORD = false>
 __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp, const double* A, const double* Bm,
                                              const double* c, const double* P, const double* p, double* Pn,
-                                             double* pn, Fac<NX, NU>& f) {
+                                             double* pn, Fac<NX, NU>& f, const double* Pown = nullptr,
+                                             const double* vpre = nullptr) {
+  static_assert(!DEC || SREORD, "DEC takes s in the SREORD order");
   constexpr int NZ = NX + NU;
   static_assert(NU == 1 || NU == 2, "NU must be 1 or 2");
   auto Pm = [&](int i, int j) { return P[symix(i, j, NX)]; };
+  double Hxx[NX * NX], Hux[NU * NX], Huu[NU * NU];
+  if constexpr (DEC) {
+#pragma unroll
+    for (int l = 0; l < NU; ++l) {
+#pragma unroll
+      for (int j = 0; j < NX; ++j) Hux[l * NX + j] = Hd[symix(j, NX + l, NZ)];
+#pragma unroll
+      for (int n = l; n < NU; ++n) Huu[l * NU + n] = Hd[symix(NX + l, NX + n, NZ)];
+    }
+  } else {
   // PA = P A, PB = P B.  Sums start from their first structural term (a product, not an
   // fma into 0.0): a model's structural ones then fold away (P * 1.0 == P exactly, while
   // fma(P, 1.0, 0.0) must be kept for the sign of zero).
@@ -65,7 +96,6 @@ __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp,
       PB[r * NU + l] = acc;
     }
   }
-  double Hxx[NX * NX], Hux[NU * NX], Huu[NU * NU];
 #pragma unroll
   for (int i = 0; i < NX; ++i)
 #pragma unroll
@@ -95,13 +125,22 @@ __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp,
       Huu[l * NU + n] = acc;
     }
   }
+  }  // !DEC
   double s[NX], gx[NX], gu[NU];
+  if constexpr (DEC) {
 #pragma unroll
-  for (int i = 0; i < NX; ++i) {
-    double acc = p[i];
+    for (int i = 0; i < NX; ++i) s[i] = vpre[i] + p[i];
+  } else if constexpr (SREORD) {
 #pragma unroll
-    for (int m = 0; m < NX; ++m) acc = fma(Pm(i, m), c[m], acc);
-    s[i] = acc;
+    for (int i = 0; i < NX; ++i) s[i] = riccati_pc_row<NX>(P, c, i) + p[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      double acc = p[i];
+#pragma unroll
+      for (int m = 0; m < NX; ++m) acc = fma(Pm(i, m), c[m], acc);
+      s[i] = acc;
+    }
   }
 #pragma unroll
   for (int i = 0; i < NX; ++i) {
@@ -137,7 +176,7 @@ __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp,
     for (int i = 0; i < NX; ++i) {
       const double ri = f.r0 * f.h0[i];
 #pragma unroll
-      for (int j = i; j < NX; ++j) Pn[symix(i, j, NX)] = fma(-ri, f.h0[j], Hxx[i * NX + j]);
+      for (int j = i; j < NX; ++j) Pn[symix(i, j, NX)] = DEC ? Pown[symix(i, j, NX)] : fma(-ri, f.h0[j], Hxx[i * NX + j]);
       pn[i] = fma(-ri, f.g0, gx[i]);
     }
   } else {
@@ -159,7 +198,8 @@ __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp,
     for (int i = 0; i < NX; ++i) {
       const double r0i = f.r0 * f.h0[i], r1i = f.r1 * f.h1[i];
 #pragma unroll
-      for (int j = i; j < NX; ++j) Pn[symix(i, j, NX)] = fma(-r1i, f.h1[j], fma(-r0i, f.h0[j], Hxx[i * NX + j]));
+      for (int j = i; j < NX; ++j)
+        Pn[symix(i, j, NX)] = DEC ? Pown[symix(i, j, NX)] : fma(-r1i, f.h1[j], fma(-r0i, f.h0[j], Hxx[i * NX + j]));
       pn[i] = fma(-r1i, f.g1, fma(-r0i, f.g0, gx[i]));
     }
   }

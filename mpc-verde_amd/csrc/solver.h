@@ -16,6 +16,9 @@ struct LinTables {
   const int32_t* tab; // N (shared) or rows x N (per instance) table indices
   int per_instance;
   int n_tab;
+  // bit j (j < 64): table j is decoupled -- B_j == 0 and no x-u block in W_j (exact zeros) --
+  // so a suffix of such stages keeps P_k across iterations (solver.hip, decoupled suffix)
+  unsigned long long dec_mask;
 };
 
 // Constants of the nonlinear ODE models (ode.h): RK4 substep, node-cost weights, model constants.

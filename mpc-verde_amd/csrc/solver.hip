@@ -21,6 +21,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "collectives.h"
 #include "models.h"
@@ -64,6 +65,16 @@ constexpr int kDiag = 12;  // counters per instance
 #endif
 
 namespace mpcx {
+
+// Model::kDecSuffix if the model declares it (linear models), false otherwise
+template <class M, class = void>
+struct DecSuffixOf {
+  static constexpr bool value = false;
+};
+template <class M>
+struct DecSuffixOf<M, std::void_t<decltype(M::kDecSuffix)>> {
+  static constexpr bool value = M::kDecSuffix;
+};
 
 // IPOPT constants (Waechter & Biegler 2006 Table 1; IPOPT defaults)
 constexpr double kEps = 2.220446049250313e-16;
@@ -179,6 +190,19 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     nbnd_l += (int)hL[i] + (int)hU[i];
   }
   const double nbound = gsum<G>((double)nbnd_l, xw);
+  // ---- decoupled suffix (linear models; riccati.h DEC).  On stages k >= kb every table is
+  //      decoupled (B = 0, no x-u Hessian block) and no state is bounded, so with delta = 0
+  //      the stage Hessian's x block, A and P_{k+1} -- hence P_k -- are the same at every
+  //      factorisation of a solve (fs is fixed after its first iteration).  Once a
+  //      factorisation with delta = 0 stored P_k in Pk (pcv), the recursion reuses it there
+  //      and only carries the vector part: the cart-pole QP's 95 move-blocked stages of
+  //      100.  kb is set at every solve's first iteration (the tables may change per step).
+  constexpr bool kDec = DecSuffixOf<Model>::value;
+  bool xfree = true;
+#pragma unroll
+  for (int i = 0; i < NX; ++i) xfree = xfree && !hL[i] && !hU[i];
+  int kb = N + 1;
+  bool pcv = false;
 
   // ---- initial point
   double z[NZ];
@@ -409,6 +433,11 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
                xw.slot, nbound, (void*)xw.buf);
 #endif
       fs = gm > 100.0 ? 100.0 / gm : 1.0;
+      if constexpr (kDec) {
+        const bool d = !hasX || (xfree && (k == N || ctx.dec));
+        kb = (int)gmax<G>(d ? -1.0 : (double)k, xw) + 1;
+        pcv = false;
+      }
       if (fs != 1.0) {  // group-uniform; given multipliers belong to the unscaled problem
 #pragma unroll
         for (int i = 0; i < NX; ++i) lam[i] *= fs;
@@ -638,15 +667,34 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
             p[i] = dl * gp[i];
           }
         }
+        // decoupled suffix: with P_{k+1} reused, s = P_{k+1} c + p_{k+1} needs only p on the
+        // chain; P_{k+1} c comes from the stored Pk of node k+1, off the chain
+        const bool reuse = kDec && pcv && delta == 0.0;  // group-uniform
+        double vpc[kDec ? NX : 1];
+        if constexpr (kDec) {
+          double Pn1[NP];
+          group_next<G, NP>(Pk, Pn1, xw);
+#pragma unroll
+          for (int i = 0; i < NX; ++i) vpc[i] = riccati_pc_row<NX>(Pn1, cdef, i);
+        }
         if constexpr (G <= 64) {
           for (int j = N - 1; j >= 0; --j) {
+            const bool cheap = reuse && j >= kb;
             double Pin_[NP], pin_[NX];
+            if (!kDec || __any(!cheap)) {
 #pragma unroll
-            for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
+              for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
+            }
 #pragma unroll
             for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
-            if (seq && k == j)
-              okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p, fac);
+            if (seq && k == j) {
+              if (cheap)  // group-uniform
+                okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, kDec, kDec>(Hd, gp, Aop, Bop, cdef, P, pin_, P, p,
+                                                                                   fac, Pk, vpc);
+              else
+                okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p,
+                                                                                     fac);
+            }
           }
         } else {  // wave by wave, N-side first; the value function crosses waves through LDS
           const int wv = (int)(threadIdx.x >> 6);
@@ -655,9 +703,12 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
               const double* in = xw.prev();  // (P, p) of node 64 (ph + 1), written last phase
               const int jtop = 64 * ph + 63;
               for (int j = min(N - 1, jtop); j >= 64 * ph; --j) {
+                const bool cheap = reuse && j >= kb;
                 double Pin_[NP], pin_[NX];
+                if (!kDec || __any(!cheap)) {
 #pragma unroll
-                for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
+                  for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
+                }
 #pragma unroll
                 for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
                 if (j == jtop && lane == 63) {
@@ -666,8 +717,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
                   for (int i = 0; i < NX; ++i) pin_[i] = in[NP + i];
                 }
-                if (seq && k == j)
-                  okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p, fac);
+                if (seq && k == j) {
+                  if (cheap)  // group-uniform
+                    okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, kDec, kDec>(Hd, gp, Aop, Bop, cdef, P, pin_, P, p,
+                                                                                       fac, Pk, vpc);
+                  else
+                    okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p,
+                                                                                         fac);
+                }
               }
               if (ph > 0 && lane == 0) {
                 double* out = xw.cur();
@@ -709,6 +766,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       status = 3;
       its = it;
     }
+    if constexpr (kDec) pcv = !failed && delta == 0.0;  // Pk now holds a delta = 0 factorisation
     riccati_gains<NX, NU>(fac, Kk, kfk);  // all lanes at once
 
     STAMP(4);

@@ -225,6 +225,35 @@ def test_pendulum_long_horizon_multiwave(mpcx, R, N):
     np.testing.assert_array_equal(r2["w"], r["w"][5:12])
 
 
+@pytest.mark.parametrize("N", [50, 100])
+def test_pendulum_decoupled_suffix_same_bits(mpcx, R, N, monkeypatch):
+    """The move-blocked stages (B = 0, no x-u cost block) reuse P_k across iterations
+    (solver.hip "decoupled suffix", riccati.h DEC).  Same solution bits, multipliers and
+    iteration counts as the full recursion (MPCX_DEC_SUFFIX=0), and the LQ oracle's solution."""
+    from mpcx import lti
+
+    lin = lti.inverted_pendulum_qp(N=N)
+    rng = np.random.default_rng(100 + N)
+    B = 48
+    scale = np.where(np.arange(B) % 3 == 0, 30.0, 1.0)[:, None]
+    x = scale * rng.uniform([-1, -.5, -.2, -.5], [1, .5, .2, .5], size=(B, 4))
+    up = rng.uniform(-50, 50, size=B)
+    P = lti.pendulum_params(lin, x, up)
+    S_fast = mpcx.nlpsol("pend", "mi355x", lin, {"ipopt": {"max_iter": 200}})
+    monkeypatch.setenv("MPCX_DEC_SUFFIX", "0")
+    S_full = mpcx.nlpsol("pend", "mi355x", lin, {"ipopt": {"max_iter": 200}})
+    a = S_fast.solve_batch(P)
+    b = S_full.solve_batch(P)
+    assert np.all(a["status"] == 0)
+    np.testing.assert_array_equal(a["iters"], b["iters"])
+    np.testing.assert_array_equal(a["w"], b["w"])
+    np.testing.assert_array_equal(a["lam_g"], b["lam_g"])
+    A, Bd = R.pendulum_model()
+    for i in range(0, B, 7):
+        u_ref = R.pendulum_qp_solve(x[i], A, Bd, N=N, uprev=up[i])
+        assert rel(a["w"][i, 5:5 + 6 * 5:6], u_ref) <= U_TOL, i
+
+
 def test_ltv_device_loop_with_device_schedule(mpcx, R):
     """Config-4 closed loop on the device: per step the stage references and the per-instance
     schedule (model re-linearised at vref[t], mpcx_set_linear_tab_dev) advance; compared with
