@@ -206,6 +206,79 @@ __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp,
   return ok;
 }
 
+// The DEC step split in two, same operations: dec_prefactor (off the chain: the factors, which
+// need no p) and dec_vector_step (on the chain: s, gx, gu and p_k); P_k is the stored one.
+template <int NX, int NU>
+__device__ __forceinline__ bool dec_prefactor(const double* Hd, Fac<NX, NU>& f) {
+  constexpr int NZ = NX + NU;
+  if constexpr (NU == 1) {
+    const double d0 = Hd[symix(NX, NX, NZ)];
+    f.r0 = rcp64(d0);
+    f.r1 = 0.0;
+    f.t = 0.0;
+    f.g1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      f.h0[j] = Hd[symix(j, NX, NZ)];
+      f.h1[j] = 0.0;
+    }
+    return d0 > 0.0;
+  } else {
+    const double a = Hd[symix(NX, NX, NZ)], b = Hd[symix(NX, NX + 1, NZ)], d = Hd[symix(NX + 1, NX + 1, NZ)];
+    const double det = fma(a, d, -b * b);
+    const double ra = rcp64(a), rdet = rcp64(det);
+    f.r0 = ra;
+    f.t = b * ra;
+    f.r1 = a * rdet;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      f.h0[j] = Hd[symix(j, NX, NZ)];
+      f.h1[j] = fma(-f.t, Hd[symix(j, NX, NZ)], Hd[symix(j, NX + 1, NZ)]);
+    }
+    return (a > 0.0) && (det > 0.0);
+  }
+}
+
+template <int NX, int NU, unsigned long long AMASK, unsigned long long BMASK>
+__device__ __forceinline__ void dec_vector_step(const double* gp, const double* A, const double* Bm, const double* vpre,
+                                                const double* p, double* pn, Fac<NX, NU>& f) {
+  double s[NX], gx[NX], gu[NU];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) s[i] = vpre[i] + p[i];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    double acc = gp[i];
+#pragma unroll
+    for (int m = 0; m < NX; ++m)
+      if (AMASK & (1ull << (m * NX + i))) acc = fma(A[m * NX + i], s[m], acc);
+    gx[i] = acc;
+  }
+#pragma unroll
+  for (int l = 0; l < NU; ++l) {
+    double acc = gp[NX + l];
+#pragma unroll
+    for (int m = 0; m < NX; ++m)
+      if (BMASK & (1ull << (m * NU + l))) acc = fma(Bm[m * NU + l], s[m], acc);
+    gu[l] = acc;
+  }
+  if constexpr (NU == 1) {
+    f.g0 = gu[0];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const double ri = f.r0 * f.h0[i];
+      pn[i] = fma(-ri, f.g0, gx[i]);
+    }
+  } else {
+    f.g0 = gu[0];
+    f.g1 = fma(-f.t, gu[0], gu[1]);
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const double r0i = f.r0 * f.h0[i], r1i = f.r1 * f.h1[i];
+      pn[i] = fma(-r1i, f.g1, fma(-r0i, f.g0, gx[i]));
+    }
+  }
+}
+
 // K = -Huu'^{-1} Hux', kf = -Huu'^{-1} gu' from the LDL^T data (off the critical path).
 template <int NX, int NU>
 __device__ __forceinline__ void riccati_gains(const Fac<NX, NU>& f, double* K, double* kf) {

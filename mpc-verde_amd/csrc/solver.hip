@@ -671,11 +671,18 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         // chain; P_{k+1} c comes from the stored Pk of node k+1, off the chain
         const bool reuse = kDec && pcv && delta == 0.0;  // group-uniform
         double vpc[kDec ? NX : 1];
+        bool okd = true;
         if constexpr (kDec) {
           double Pn1[NP];
           group_next<G, NP>(Pk, Pn1, xw);
 #pragma unroll
           for (int i = 0; i < NX; ++i) vpc[i] = riccati_pc_row<NX>(Pn1, cdef, i);
+          // reused stages: factors and P_k set here, off the chain (dec_prefactor)
+          if (reuse && k >= kb && k < N) {
+            okd = dec_prefactor<NX, NU>(Hd, fac);
+#pragma unroll
+            for (int i = 0; i < NP; ++i) P[i] = Pk[i];
+          }
         }
         if constexpr (G <= 64) {
           for (int j = N - 1; j >= 0; --j) {
@@ -688,9 +695,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
             for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
             if (seq && k == j) {
-              if (cheap)  // group-uniform
-                okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, kDec, kDec>(Hd, gp, Aop, Bop, cdef, P, pin_, P, p,
-                                                                                   fac, Pk, vpc);
+              if (cheap) {  // group-uniform
+                dec_vector_step<NX, NU, Model::AMASK, Model::BMASK>(gp, Aop, Bop, vpc, pin_, p, fac);
+                okl = okd;
+              }
               else
                 okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p,
                                                                                      fac);
@@ -718,9 +726,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
                   for (int i = 0; i < NX; ++i) pin_[i] = in[NP + i];
                 }
                 if (seq && k == j) {
-                  if (cheap)  // group-uniform
-                    okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, kDec, kDec>(Hd, gp, Aop, Bop, cdef, P, pin_, P, p,
-                                                                                       fac, Pk, vpc);
+                  if (cheap) {  // group-uniform
+                    dec_vector_step<NX, NU, Model::AMASK, Model::BMASK>(gp, Aop, Bop, vpc, pin_, p, fac);
+                    okl = okd;
+                  }
                   else
                     okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p,
                                                                                          fac);
