@@ -14,6 +14,16 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 REL_TOL = 1e-4  # north_star: optimal (x*, u*) within 1e-4 relative of CasADi/IPOPT
+# An instance whose optimum differs from the same-algorithm C++ oracle's is certified instead:
+# complex-step KKT residual (projected Lagrangian gradient, defects) of the returned point
+# at most KKT_CERT_TOL, objective no worse than the oracle's.  The counts of such instances
+# are bounded per test and printed (run with -s).  Measured on MI355X (round 2): every bound
+# below is met with 0 differing instances, so each is 0.
+KKT_CERT_TOL = 1e-8
+MAX_CONFIG2_MISMATCH = 0  # of 1024 config-2 instances
+MAX_HORIZON_MISMATCH = {}  # N -> allowed certified mismatches in test_horizons (none)
+MAX_FIXTURE_MISMATCH = 0  # of the 32 committed N=20 oracle optima (independent algorithm)
+MAX_ITER_MISMATCH = 0  # iteration counts vs the C++ IPOPT restatement, of 1024, cold and warm
 
 
 def rel_err(a, b):
@@ -190,10 +200,17 @@ def test_config2_batch_vs_cpp_oracle(mpcx, R, C, golden):
     ref = C.solve_batch(rocp, P, w0=w0, nthreads=0)
     assert np.all(ref["status"] == 0)
     errs = np.array([rel_err(r["w"][b], ref["w"][b]) for b in range(1024)])
-    # same algorithm, same start: the same local optimum for (nearly) every instance
-    assert np.mean(errs <= REL_TOL) >= 0.99, np.sort(errs)[-10:]
-    # objective never worse than the oracle's by more than round-off where they differ
-    assert np.all(r["f"] <= ref["f"] * (1 + 1e-6) + 1e-9) or np.mean(errs <= REL_TOL) >= 0.99
+    # same algorithm, same start: the same local optimum for every instance.  An instance
+    # that differs is reported by count and must be certified: a KKT point of the NLP
+    # (complex-step Lagrangian gradient projected on the bounds, and the defects) whose
+    # objective is no worse than the oracle's.
+    diff = np.flatnonzero(errs > REL_TOL)
+    print(f"config 2: {diff.size} of 1024 instances differ from the C++ oracle by > {REL_TOL:g}")
+    assert diff.size <= MAX_CONFIG2_MISMATCH, (diff.size, np.sort(errs)[-10:])
+    for b in diff:
+        pg, cv = R.kkt_residual_ms(r["w"][b], r["lam_g"][b], P[b], rocp)
+        assert pg <= KKT_CERT_TOL and cv <= KKT_CERT_TOL, (b, pg, cv)
+        assert r["f"][b] <= ref["f"][b] * (1 + 1e-9), (b, r["f"][b], ref["f"][b])
     # independent numpy oracle on a sample (projected Newton, single shooting)
     for b in list(range(0, 84, 12)) + list(range(84, 1024, 157)):
         wn, info = R.solve_ms(P[b], rocp)
@@ -241,9 +258,16 @@ def test_horizons(mpcx, C, R, N):
     rocp = R.UnicycleOCP(N=N)
     X = np.repeat(P[:, None, 0:3], N + 1, axis=1)
     ref = C.solve_batch(rocp, P, w0=R.join_w(X, np.zeros((16, N, 2))))
-    ok = [rel_err(r["w"][b], ref["w"][b]) <= REL_TOL for b in range(16) if ref["status"][b] == 0]
-    assert np.all(r["status"] == 0)
-    assert np.mean(ok) >= 0.9
+    assert np.all(r["status"] == 0) and np.all(ref["status"] == 0)
+    errs = np.array([rel_err(r["w"][b], ref["w"][b]) for b in range(16)])
+    diff = np.flatnonzero(errs > REL_TOL)
+    print(f"N={N}: {diff.size} of 16 instances differ from the C++ oracle by > {REL_TOL:g}")
+    for b in diff:  # certified: a KKT point no worse than the oracle's
+        pg, cv = R.kkt_residual_ms(r["w"][b], r["lam_g"][b], P[b], rocp)
+        print(f"  instance {b}: err {errs[b]:.2e} kkt {pg:.2e} cv {cv:.2e} f {r['f'][b]:.12g} oracle {ref['f'][b]:.12g}")
+        assert pg <= KKT_CERT_TOL and cv <= KKT_CERT_TOL, (b, pg, cv)
+        assert r["f"][b] <= ref["f"][b] * (1 + 1e-9), (b, r["f"][b], ref["f"][b])
+    assert diff.size <= MAX_HORIZON_MISMATCH.get(N, 0), diff
 
 
 @pytest.mark.parametrize("N,B", [(10, 40), (20, 37), (40, 9), (100, 5)])
@@ -320,6 +344,60 @@ def test_single_shooting_formulation(mpcx, R, golden):
     sol = solver(x0=[0] * (2 * N), lbx=lbw, ubx=ubw, lbg=-math.inf, ubg=math.inf, p=[0, 0, 0, 10, 10, 0])
     assert sol["x"].shape == (2 * N, 1) and sol["g"].shape == (2 * N, 1)
     assert rel_err(sol["x"][0:2, 0], rows2[0, 3:5]) <= REL_TOL
+
+
+def test_single_shooting_closed_loop_2exemplo(mpcx, golden):
+    """The reference's single-shooting driver loop (Casadi/single_shooting_v2.py:201-266) with
+    ca.nlpsol swapped for mpcx.nlpsol(formulation='single_shooting'): the U-only warm start
+    shifted each step (:245-249), the plant F (:242), the predicted rollout (:221-224); it
+    reproduces 2exemplo.xlsx -- 84 solves, states < 1e-6, controls <= 1e-4 relative -- and the
+    export table of :284-301 row for row."""
+    rows = np.array(golden["single_shooting"]["rows"])
+    N, T = 10, 0.2
+    ocp = mpcx.unicycle_point_to_point(N=N, formulation="single_shooting")
+    solver = mpcx.nlpsol("solver", "mi355x", ocp, {"ipopt": {"max_iter": 2000, "print_level": 0,
+                                                                "acceptable_tol": 1e-8,
+                                                                "acceptable_obj_change_tol": 1e-6},
+                                                    "print_time": 0})
+    F = mpcx.integrator(mpcx.unicycle_point_to_point(N=N))
+    lbw, ubw = [], []
+    for _ in range(N):
+        lbw += [-1, -math.pi / 4]
+        ubw += [1, math.pi / 4]
+    args = {"lbg": -math.inf, "ubg": math.inf, "lbx": lbw, "ubx": ubw}
+    state_init = np.array([0.0, 0.0, 0.0])
+    state_target = np.array([10.0, 10.0, 0.0])
+    w0 = [0.0] * (2 * N)
+    log = mpcx.ClosedLoopLog.for_ocp(mpcx.unicycle_point_to_point(N=N), state_init)
+    mpc_iter, t0 = 0, 0.0
+    states, controls = [], []
+    while np.linalg.norm(state_init - state_target) > 1e-1 and mpc_iter * T < 20:
+        args["p"] = np.concatenate([state_init, state_target])
+        sol = solver(x0=w0, lbx=args["lbx"], ubx=args["ubx"], lbg=args["lbg"], ubg=args["ubg"], p=args["p"])
+        assert sol["x"].shape == (2 * N, 1) and solver.stats()["success"]
+        u = sol["x"][:, 0].reshape(N, 2).T  # ca.reshape(sol['x'], n_controls, N)
+        X1, Xs = state_init, [state_init]
+        for k in range(N):  # predicted rollout X1 = F([X1; target], u[:, k])[0]
+            X1 = F(np.concatenate([X1, state_target]), u[:, k])[0].reshape(-1)
+            Xs.append(X1)
+        w_ms = np.concatenate([Xs[0]] + [np.concatenate([u[:, k], Xs[k + 1]]) for k in range(N)])
+        log.record(w_ms, t0)
+        states.append(state_init.copy())
+        controls.append(u[:, 0].copy())
+        t0 += T
+        state_init = F(args["p"], u[:, 0])[0].reshape(-1)
+        w0 = np.hstack([u[:, 1:], u[:, -1:]]).T.reshape(-1)  # ca.reshape(u0, n_controls*N, 1)
+        mpc_iter += 1
+    assert mpc_iter == 84
+    states, controls = np.array(states), np.array(controls)
+    assert np.max(np.abs(states - rows[1:85, 0:3])) < 1e-6
+    assert rel_err(controls, rows[0:84, 3:5]) <= REL_TOL
+    tab = log.table()
+    got = np.stack([tab[c] for c in ("x", "y", "theta", "v", "w", "t")], axis=1)
+    assert got.shape == rows.shape
+    assert np.max(np.abs(got[:, 0:3] - rows[:, 0:3])) < 1e-6
+    assert rel_err(got[:, 3:5], rows[:, 3:5]) <= REL_TOL
+    np.testing.assert_allclose(got[:, 5], rows[:, 5], atol=1e-12)
 
 
 # ----------------------------------------------------------------------------- warm start
@@ -523,14 +601,22 @@ def test_n20_vs_committed_oracle_optima(mpcx):
 
     from conftest import ROOT
 
+    from oracle import nlp_ref
+
     fx = np.load(os.path.join(ROOT, "tests", "golden", "unicycle_N20_oracle.npz"))
     solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=20))
     r = solver.solve_batch(fx["P"])
     assert np.all(r["status"] == 0)
-    same = [abs(r["f"][b] - fx["J"][b]) <= 1e-6 * max(1.0, abs(fx["J"][b])) for b in range(len(fx["J"]))]
-    assert np.mean(same) >= 0.9  # non-convex: an instance may settle in another local optimum
-    for b in np.flatnonzero(same):
-        assert rel_err(r["w"][b], fx["w"][b]) <= REL_TOL, b
+    B = len(fx["J"])
+    errs = np.array([rel_err(r["w"][b], fx["w"][b]) for b in range(B)])
+    diff = np.flatnonzero(errs > REL_TOL)
+    print(f"N=20 fixture: {diff.size} of {B} instances differ from the committed oracle optima by > {REL_TOL:g}")
+    rocp = nlp_ref.UnicycleOCP(N=20)
+    for b in diff:  # non-convex NLP, independent algorithm: certified KKT point instead
+        pg, cv = nlp_ref.kkt_residual_ms(r["w"][b], r["lam_g"][b], fx["P"][b], rocp)
+        print(f"  instance {b}: err {errs[b]:.2e} kkt {pg:.2e} cv {cv:.2e} f {r['f'][b]:.12g} oracle {fx['J'][b]:.12g}")
+        assert pg <= KKT_CERT_TOL and cv <= KKT_CERT_TOL, (b, pg, cv)
+    assert diff.size <= MAX_FIXTURE_MISMATCH, diff
 
 
 def test_rk4_sens_ragged_tiles(mpcx):
@@ -738,7 +824,9 @@ def test_iteration_counts_match_cpp_oracle(mpcx, R, C):
     r = solver.solve_batch(P)
     rocp = R.UnicycleOCP(N=N)
     ref = C.solve_batch(rocp, P, w0=bench._cold(P, N, R), nthreads=0)
-    assert np.mean(r["iters"] == ref["iters"]) >= 0.99
+    n1 = int(np.sum(r["iters"] != ref["iters"]))
+    print(f"cold: {n1} of {B} iteration counts differ from the C++ oracle")
+    assert n1 <= MAX_ITER_MISMATCH, np.flatnonzero(r["iters"] != ref["iters"])
     # one closed-loop step later, warm-started from the shifted primal-dual solution
     P2 = P.copy()
     P2[:, 0:3], _ = R.F(P[:, 0:3], r["w"][:, 3:5], P[:, 3:6], rocp)
@@ -746,4 +834,6 @@ def test_iteration_counts_match_cpp_oracle(mpcx, R, C):
     r2 = solver.solve_batch(P2, w0=w0, lam_g0=l0, lam_x0=lx0)
     ref2 = C.solve_batch_warm(rocp, P2, w0, lam0=l0, lamx0=lx0, mu_init=1e-4, bound_push=1e-4, mult_push=1e-4,
                               nthreads=0)
-    assert np.mean(r2["iters"] == ref2["iters"]) >= 0.99
+    n2 = int(np.sum(r2["iters"] != ref2["iters"]))
+    print(f"warm: {n2} of {B} iteration counts differ from the C++ oracle")
+    assert n2 <= MAX_ITER_MISMATCH, np.flatnonzero(r2["iters"] != ref2["iters"])
