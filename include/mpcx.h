@@ -122,6 +122,9 @@ int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N);
 int mpcx_create(const mpcx_spec* s, mpcx_handle** h);
 void mpcx_destroy(mpcx_handle* h);
 const char* mpcx_last_error(void);
+/* Build identity: a hash of the sources the library was compiled from (no reference
+   counterpart; mpcx/_lib.py refuses a libmpcx.so whose hash differs from the tree's). */
+const char* mpcx_source_hash(void);
 
 /* Tables of an MPCX_MODEL_LINEAR handle (host pointers, copied to the device):
  *   A n_tab x nx x nx, B n_tab x nx x nu, c n_tab x nx (may be NULL = 0),
@@ -144,8 +147,10 @@ int mpcx_dims(const mpcx_handle* h, int32_t* n_w, int32_t* n_g, int32_t* n_p);
 
 /* Batched NLP solve (host pointers, synchronous).
  *   P      B x n_p parameters (layout per spec.param_layout)
- *   w0     B x n_w initial guesses, or NULL = cold start (X_k = x0, U_k = 0,
- *          the reference's repmat(state_init) / zeros initialisation, :212-213)
+ *   w0     B x n_w initial guesses, or NULL = cold start (X_k = x0, U_k = 0: the
+ *          feasible guess X0 = repmat(state_init), u0 = zeros that the script builds at
+ *          :212-213; its own first solve passes the all-zero w0 of :118-169, which equals
+ *          this guess for its state_init = 0, and later solves pass the shifted guess)
  *   lam_g0 B x n_g, lam_x0 B x n_w: initial multipliers (CasADi's lam_g0 /
  *          lam_x0 solver inputs), or NULL.  If either is given the solve starts
  *          as IPOPT's warm_start_init_point (spec.warm_*); otherwise as IPOPT's
@@ -191,7 +196,7 @@ int mpcx_shift_dev(mpcx_handle* h, int32_t B, double* d_P, const double* d_w, do
  *   d_P[:, 0:nx]  <- F(x0, u_0*)                      (plant, :273)
  *   d_w0          <- solution shifted by one interval  (warm start of the next step)
  *   d_lam_g0/d_lam_x0 <- multipliers shifted alike (may be NULL: not kept)
- * flags: MPCX_STEP_COLD -- ignore d_w0 / multipliers on input (cold start, :212-213);
+ * flags: MPCX_STEP_COLD -- ignore d_w0 / multipliers on input (cold start, see w0 above);
  *        MPCX_STEP_PRIMAL_ONLY -- warm primal start, default multiplier initialisation.
  * Otherwise the solve starts from d_w0 and (if given) the shifted multipliers as IPOPT's
  * warm_start_init_point.  Solution outputs as in mpcx_solve_batch_dev (d_w_out required). */

@@ -205,7 +205,10 @@ int check_bounds_vec(const mpcx_handle* h, const double* lbw, const double* ubw)
   for (int i = 0; i < h->nw; ++i) {
     const double l = lbw ? lbw[i] : -1e20, u = ubw ? ubw[i] : 1e20;
     if (std::isnan(l) || std::isnan(u) || l > u) return fail(MPCX_EINVAL, "lbw/ubw: NaN or lb > ub at index " + std::to_string(i));
-    if (l == u && l > -1e19) return fail(MPCX_EINVAL, "lbw == ubw (fixed variable) is not supported, index " + std::to_string(i));
+    // X_0 (i < nx) is pinned by g_0 and its bounds are replaced by +-inf (mpcx_solve_batch), so
+    // a caller fixing it through lbx = ubx (CasADi style) is accepted
+    if (l == u && l > -1e19 && i >= h->spec.nx)
+      return fail(MPCX_EINVAL, "lbw == ubw (fixed variable) is not supported, index " + std::to_string(i));
   }
   return 0;
 }
@@ -214,6 +217,16 @@ int check_bounds_vec(const mpcx_handle* h, const double* lbw, const double* ubw)
 extern "C" {
 
 const char* mpcx_last_error(void) { return g_err.c_str(); }
+
+// hash of the sources this library was built from (Makefile: MPCX_SRC_HASH); the loader
+// (mpcx/_lib.py) refuses a library whose hash differs from the tree's
+const char* mpcx_source_hash(void) {
+#ifdef MPCX_SRC_HASH
+  return MPCX_SRC_HASH;
+#else
+  return "unknown";
+#endif
+}
 
 int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N) {
   if (!s) return fail(MPCX_EINVAL, "null spec");

@@ -29,7 +29,8 @@ STATUS = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Maximum_Ite
 # C-ABI entry points (include/mpcx.h) -- checked by tests/test_capi_symbols.py
 EXPORTS = ("mpcx_default_spec", "mpcx_create", "mpcx_destroy", "mpcx_last_error", "mpcx_dims", "mpcx_solve_batch",
            "mpcx_solve_batch_dev", "mpcx_plant_step", "mpcx_shift_dev", "mpcx_rk4_sens", "mpcx_rk4_sens_dev",
-           "mpcx_set_linear_model", "mpcx_set_linear_tab_dev", "mpcx_step_dev", "mpcx_run_dev")
+           "mpcx_set_linear_model", "mpcx_set_linear_tab_dev", "mpcx_step_dev", "mpcx_run_dev",
+           "mpcx_source_hash")
 STEP_COLD = 1
 STEP_PRIMAL_ONLY = 2
 
@@ -77,8 +78,29 @@ def _bind_single_hip_runtime():
         ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
 
 
+def source_hash():
+    """Hash of the library's sources in the tree, computed as mpc-verde_amd/Makefile does
+    (SRC, then the sorted csrc/*.h, then include/mpcx.h; sha256, 16 hex digits), or None
+    when the sources are not next to the package (an installed copy)."""
+    import glob
+    import hashlib
+
+    pkg = os.path.dirname(_HERE)
+    files = [os.path.join(pkg, "csrc", "solver.hip"), os.path.join(pkg, "csrc", "capi.cpp")]
+    files += sorted(glob.glob(os.path.join(pkg, "csrc", "*.h")))
+    files.append(os.path.join(os.path.dirname(pkg), "include", "mpcx.h"))
+    if not all(os.path.exists(f) for f in files):
+        return None
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def load():
-    """Load libmpcx.so (raises if it has not been built)."""
+    """Load libmpcx.so (raises if it has not been built, or was built from other sources
+    than the tree's -- a stale binary must not run as the product)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -109,6 +131,11 @@ def load():
                                  vp, vp, vp, vp]
     for name in EXPORTS:
         getattr(lib, name)  # AttributeError if an export is missing
+    lib.mpcx_source_hash.restype = ctypes.c_char_p
+    built, tree = lib.mpcx_source_hash().decode(), source_hash()
+    if tree is not None and built != tree and os.environ.get("MPCX_ALLOW_STALE_LIB") != "1":
+        raise MpcxError(f"{LIB_PATH} was built from other sources (hash {built}) than the tree's ({tree}): "
+                        "rebuild it with `make -C mpc-verde_amd`")
     _lib = lib
     return lib
 

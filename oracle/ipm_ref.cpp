@@ -6,7 +6,7 @@
 // cpu_baseline leg -- as the checker and as the timed CPU baseline, never as
 // the product.  Parity: pinned against tests/golden/unicycle_N10_golden.json
 // (the reference's own CasADi+IPOPT outputs) and against oracle/nlp_ref.py in
-// tests/test_oracle_cpp.py.
+// tests/test_oracle.py.
 //
 // What it restates (paths relative to /root/reference):
 //   NLP     Casadi/multiple_shooting_casadi.py:68-114 (unicycle f, L, RK4 with

@@ -40,6 +40,20 @@ def test_library_exports_every_declared_symbol(lib):
         assert re.search(rf"\bT {s}$", out, re.M), s
 
 
+def test_library_matches_tree_sources(lib, monkeypatch):
+    """The built library embeds the hash of the sources it was compiled from; the loader
+    refuses one whose hash differs from the tree's (a stale .so must not run as the product)."""
+    from mpcx import _lib
+
+    lib.mpcx_source_hash.restype = ctypes.c_char_p
+    assert lib.mpcx_source_hash().decode() == _lib.source_hash()
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "source_hash", lambda: "0000000000000000")
+    monkeypatch.setattr(_lib, "_bind_single_hip_runtime", lambda: None)
+    with pytest.raises(_lib.MpcxError, match="other sources"):
+        _lib.load()
+
+
 def test_library_targets_gfx950():
     """The shared library embeds a gfx950 code object (HIP fat binary)."""
     data = open(LIB, "rb").read()

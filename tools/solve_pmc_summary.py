@@ -61,8 +61,6 @@ def main():
         if t:
             r["fp64_tflops"] = round(flops / t / 1e12, 3)
             r["fp64_frac_of_peak"] = round(flops / t / 1e12 / PEAK_FP64_TFLOPS, 4)
-            if cb.get("GRBM_GUI_ACTIVE"):
-                r["effective_clock_ghz"] = round(cb["GRBM_GUI_ACTIVE"] / 8 / t / 1e9, 3)
         res[k] = r
     print(json.dumps(res, indent=1))
 
