@@ -1,1426 +1,18 @@
-// solver.hip -- fused batched interior-point solve of multiple-shooting MPC NLPs on gfx950
-// (MI355X), plus the RK4+Jacobian sweep, plant and shift kernels.
+// solver.hip -- model dispatch of the fused solve (kernels.h, one translation unit per model:
+// solve_<model>.hip) and the RK4+Jacobian sweep kernel over B x N unicycle intervals.
 //
 // Replaces, for B independent instances at once, the reference's
 //   sol = solver(x0=w0, lbx, ubx, lbg, ubg, p)     Casadi/multiple_shooting_casadi.py:235-242
-// where solver = ca.nlpsol('solver', 'ipopt', prob, opts) (:181-197) -- IPOPT's primal-dual
-// barrier method (Waechter & Biegler 2006) on the NLP of :116-178 -- and the mpctools
-// nmpc/QP solves of Trajectory_tracking.py:72,107 and inverted_pendulum_...py:64,74.
-//
-// Execution model: one *lane group* of G = 16/32/64 lanes per instance;
-// lane k owns shooting node k: X_k, U_k, the defect of interval k, its multipliers, bound
-// duals, the stage derivative blocks (A_k, B_k, g_k, H_k, all in VGPRs) and its Riccati
-// data.  The whole solve -- evaluation sweep, KKT Riccati factor/solve, fraction-to-
-// boundary, filter line search, barrier update -- runs inside ONE launch; nothing but the
-// inputs and the solution touch HBM.  Node-parallel work runs on all lanes; the Riccati
-// recursion and the forward roll-out are the sequential critical path and carry only
-// what the next node needs (value function, state step) lane to lane by DPP.  Per-
-// instance scalars are symmetric group reductions (bit-identical on every lane).  Every
-// loop is wave-uniform; lanes of finished instances are predicated.
+// (DESIGN.md §3), and the function + Jacobian evaluations IPOPT requests from CasADi (§4).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <cstdint>
-#include <type_traits>
 
-#include "collectives.h"
-#include "models.h"
-#include "ode.h"
-#include "pscan.h"
-#include "riccati.h"
 #include "solver.h"
-
-// Diagnostic build only (-DMPCX_STAMPS, `make stamps`): per-phase s_memtime cycle
-// accounting of the solve loop (cdna_hip_programming.md §7 "In-kernel stamps").
-#ifdef MPCX_STAMPS
-__device__ unsigned long long* g_mpcx_stamps = nullptr;
-// per-instance event counters (diagnostic build; indices at the kernel's `diag` array)
-__device__ int* g_mpcx_diag = nullptr;
-constexpr int kDiag = 12;  // counters per instance
-#define DIAG(i) (++diag[(i)])
-#define DIAG_IF(c, i) \
-  do {                \
-    if (c) ++diag[(i)]; \
-  } while (0)
-#define STAMP(p)                                                                \
-  do {                                                                          \
-    __builtin_amdgcn_sched_barrier(0);                                          \
-    unsigned long long t_;                                                      \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-    __builtin_amdgcn_sched_barrier(0);                                          \
-    st_acc[st_ph] += t_ - st_last;                                              \
-    st_last = t_;                                                               \
-    st_ph = (p);                                                                \
-  } while (0)
-#else
-#define STAMP(p) \
-  do {           \
-  } while (0)
-#define DIAG(i) \
-  do {          \
-  } while (0)
-#define DIAG_IF(c, i) \
-  do {                \
-  } while (0)
-#endif
+#include "unicycle.h"
 
 namespace mpcx {
-
-// Model::kDecSuffix if the model declares it (linear models), false otherwise
-template <class M, class = void>
-struct DecSuffixOf {
-  static constexpr bool value = false;
-};
-template <class M>
-struct DecSuffixOf<M, std::void_t<decltype(M::kDecSuffix)>> {
-  static constexpr bool value = M::kDecSuffix;
-};
-
-// IPOPT constants (Waechter & Biegler 2006 Table 1; IPOPT defaults)
-constexpr double kEps = 2.220446049250313e-16;
-constexpr double kKappaEps = 10.0, kKappaMu = 0.2, kThetaMu = 1.5, kTauMin = 0.99;
-constexpr double kKappaSigma = 1e10, kSmax = 100.0;
-constexpr double kGammaTheta = 1e-5, kGammaPhi = 1e-8, kDeltaSw = 1.0, kSTheta = 1.1, kSPhi = 2.3;
-constexpr double kEtaPhi = 1e-8, kGammaAlpha = 0.05;
-constexpr double kDw0 = 1e-4, kDwMin = 1e-20, kDwMax = 1e40, kKwMinus = 1.0 / 3, kKwPlus = 8, kKwPlusBar = 100;
-constexpr double kBoundPush = 1e-2, kBoundFrac = 1e-2, kInfBound = 1e19;
-constexpr int kFilterResetTrigger = 5, kMaxFilterResets = 5;  // IPOPT filter_reset_trigger, max_filter_resets
-
-// interleaved reference layout w = [X_0 | U_0 X_1 | ... | U_{N-1} X_N]
-template <int NX, int NU>
-__device__ __forceinline__ int ixw(int k, int i) {
-  return k == 0 ? i : NX + (NX + NU) * (k - 1) + NU + i;
-}
-template <int NX, int NU>
-__device__ __forceinline__ int iuw(int k, int i) {
-  return NX + (NX + NU) * k + i;
-}
-
-// sum of log(slack) over the bounded components of a lane's variables as ONE log: the
-// product of the slacks' frexp mantissas (each in [0.5, 1), at most 2 NZ factors, so no
-// under/overflow) plus the exponents times ln 2.  One log instead of one per bound.
-template <int NZ>
-__device__ __forceinline__ double barrier_logsum(const double* z, const double* lb, const double* ub, const bool* hL,
-                                                 const bool* hU) {
-  double m = 1.0;
-  int e = 0;
-#pragma unroll
-  for (int i = 0; i < NZ; ++i) {
-    int el, eu;
-    const double ml = frexp(z[i] - lb[i], &el), mu = frexp(ub[i] - z[i], &eu);
-    m *= hL[i] ? ml : 1.0;
-    e += hL[i] ? el : 0;
-    m *= hU[i] ? mu : 1.0;
-    e += hU[i] ? eu : 0;
-  }
-  return log(m) + (double)e * 0.69314718055994530942;
-}
-
-#ifndef MPCX_WAVES_PER_EU
-#define MPCX_WAVES_ATTR
-#else
-#define MPCX_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(MPCX_WAVES_PER_EU, MPCX_WAVES_PER_EU)))
-#endif
-template <class Model, int G>
-__global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(SolveArgs a) {
-  constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2, NP = NX * (NX + 1) / 2;
-  static_assert(NP + NX <= kXchStride && 2 * NZ + NX <= kXchStride && NX * NX + NX <= kXchStride,
-                "LDS exchange slot too small");
-  const int lane = threadIdx.x & 63;
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int k = (int)(gid & (G - 1));  // node of this lane
-  // multi-wave groups (G > 64, one workgroup per instance) exchange through LDS
-  __shared__ double xch[2 * XWave<G>::W * kXchStride];
-  // LDS buffer of the Riccati scan (pscan.h): one element per thread, structure of arrays
-  constexpr int kSBS = G > 64 ? G : 64;  // threads per block = field stride
-  __shared__ double sbuf[Model::kParallelRiccati ? RElem<NX>::NE * kSBS : 1];
-  // LDS cache of the ODE models' transcendental values across their derivative passes (ode.h)
-  __shared__ double tcache[Model::kTrigSlots > 0 ? Model::kTrigSlots * kSBS : 1];
-  XWave<G> xw{xch, 0};
-  const int inst = (int)(gid / G);
-  const bool valid = inst < a.B;
-  const int N = a.N;
-  const int nw = NX + NZ * N, ng = NX * (N + 1);
-  const bool hasX = valid && k <= N;
-  const bool hasU = valid && k < N;
-
-  // ---- per-instance parameters and per-node model context
-  double x0[NX];
-#pragma unroll
-  for (int i = 0; i < NX; ++i) x0[i] = 0.0;
-  const double* Pin = a.P + (size_t)(valid ? inst : 0) * a.p_stride;
-  if (valid)
-#pragma unroll
-    for (int i = 0; i < NX; ++i) x0[i] = Pin[i];
-  const ModelArgs ma = [&] {
-    ModelArgs m = model_args(a);
-    if (Model::kTrigSlots > 0) {
-      m.tc = tcache + threadIdx.x;
-      m.tc_stride = kSBS;
-    }
-    return m;
-  }();
-  typename Model::Ctx ctx;
-  Model::load_ctx(ma, valid ? inst : 0, Pin, k, hasU, ctx);
-
-  // ---- bounds of my variables z = (x_k, u_k); x_0 is free (pinned by g_0)
-  double lb[NZ], ub[NZ];
-  bool hL[NZ], hU[NZ];
-#pragma unroll
-  for (int i = 0; i < NZ; ++i) {
-    lb[i] = -1e20;
-    ub[i] = 1e20;
-  }
-  if (hasX && k > 0)
-    for (int i = 0; i < NX; ++i) {
-      lb[i] = a.lbw[ixw<NX, NU>(k, i)];
-      ub[i] = a.ubw[ixw<NX, NU>(k, i)];
-    }
-  if (hasU)
-    for (int i = 0; i < NU; ++i) {
-      lb[NX + i] = a.lbw[iuw<NX, NU>(k, i)];
-      ub[NX + i] = a.ubw[iuw<NX, NU>(k, i)];
-    }
-  int nbnd_l = 0;
-#pragma unroll
-  for (int i = 0; i < NZ; ++i) {
-    const bool own = (i < NX) ? hasX : hasU;
-    hL[i] = own && lb[i] > -kInfBound;
-    hU[i] = own && ub[i] < kInfBound;
-    nbnd_l += (int)hL[i] + (int)hU[i];
-  }
-  const double nbound = gsum<G>((double)nbnd_l, xw);
-  // ---- decoupled suffix (linear models; riccati.h DEC).  On stages k >= kb every table is
-  //      decoupled (B = 0, no x-u Hessian block) and no state is bounded, so with delta = 0
-  //      the stage Hessian's x block, A and P_{k+1} -- hence P_k -- are the same at every
-  //      factorisation of a solve (fs is fixed after its first iteration).  Once a
-  //      factorisation with delta = 0 stored P_k in Pk (pcv), the recursion reuses it there
-  //      and only carries the vector part: the cart-pole QP's 95 move-blocked stages of
-  //      100.  kb is set at every solve's first iteration (the tables may change per step).
-  constexpr bool kDec = DecSuffixOf<Model>::value;
-  bool xfree = true;
-#pragma unroll
-  for (int i = 0; i < NX; ++i) xfree = xfree && !hL[i] && !hU[i];
-  int kb = N + 1;
-  bool pcv = false;
-
-  // ---- initial point
-  double z[NZ];
-#pragma unroll
-  for (int i = 0; i < NZ; ++i) z[i] = 0.0;
-  if (hasX) {
-    if (a.w0) {
-      const double* w0 = a.w0 + (size_t)inst * nw;
-      for (int i = 0; i < NX; ++i) z[i] = w0[ixw<NX, NU>(k, i)];
-      if (hasU)
-        for (int i = 0; i < NU; ++i) z[NX + i] = w0[iuw<NX, NU>(k, i)];
-    } else {
-#pragma unroll
-      for (int i = 0; i < NX; ++i) z[i] = x0[i];  // repmat(state_init), U = 0
-    }
-  }
-  // bound push (IPOPT bound_push / bound_frac = 1e-2; warm start: warm_start_bound_push)
-  bool warm = a.warm != 0;
-  double lx0[NZ];  // given bound multipliers (zU - zL) of my variables
-#pragma unroll
-  for (int i = 0; i < NZ; ++i) lx0[i] = 0.0;
-  if (warm && a.lamx0 && hasX) {
-    const double* l = a.lamx0 + (size_t)inst * nw;
-    if (k > 0)
-      for (int i = 0; i < NX; ++i) lx0[i] = l[ixw<NX, NU>(k, i)];
-    if (hasU)
-      for (int i = 0; i < NU; ++i) lx0[NX + i] = l[iuw<NX, NU>(k, i)];
-  }
-  double zL[NZ], zU[NZ];
-  // starting point of one solve from z (primal guess) and lx0 (given zU - zL): IPOPT's
-  // bound push and dual initialisation -- shared by the launch start and the warm restarts
-  // of multi-step launches, so both give the same bits
-  auto init_point = [&]() __attribute__((always_inline)) {
-    const double push = warm ? a.bound_push : kBoundPush, frac = warm ? a.bound_push : kBoundFrac;
-#pragma unroll
-    for (int i = 0; i < NZ; ++i) {
-      if (hL[i] && hU[i]) {
-        const double pl = fmin(push * fmax(1.0, fabs(lb[i])), frac * (ub[i] - lb[i]));
-        const double pu = fmin(push * fmax(1.0, fabs(ub[i])), frac * (ub[i] - lb[i]));
-        z[i] = fmin(fmax(z[i], lb[i] + pl), ub[i] - pu);
-      } else if (hL[i]) {
-        z[i] = fmax(z[i], lb[i] + push * fmax(1.0, fabs(lb[i])));
-      } else if (hU[i]) {
-        z[i] = fmin(z[i], ub[i] - push * fmax(1.0, fabs(ub[i])));
-      }
-      zL[i] = hL[i] ? (warm ? fmax(-lx0[i], a.mult_push) : 1.0) : 0.0;
-      zU[i] = hU[i] ? (warm ? fmax(lx0[i], a.mult_push) : 1.0) : 0.0;
-    }
-  };
-  init_point();
-  double lam[NX];  // lambda_k: multiplier of g_k (the constraint defining X_k)
-#pragma unroll
-  for (int i = 0; i < NX; ++i) lam[i] = (warm && a.lam0 && hasX) ? a.lam0[(size_t)inst * ng + NX * k + i] : 0.0;
-
-  // ---- stage evaluation (all lanes evaluate -- SIMD, no extra cost -- lanes without an
-  //      interval mask the results; A and B keep their structural constants)
-  double xf[NX], qv, A[NX * NX], Bm[NX * NU], gq[NZ], Hs[NH];
-  double cdef[NX], c0[NX];  // cdef = F(X_k,U_k) - X_{k+1} (constraint k+1), c0 = x0 - X_0 (lane 0)
-  double fs = 1.0;
-  // evaluation at the point (zz, ll): also the line search's first trial when the model's
-  // kEvalInSearch is set
-  auto eval_at = [&](const double* zz, const double* ll) __attribute__((always_inline)) {
-    double ln[NX], xn[NX], own[2 * NX], nxt[2 * NX];
-#pragma unroll
-    for (int i = 0; i < NX; ++i) {
-      own[i] = ll[i];
-      own[NX + i] = zz[i];
-    }
-    group_next<G, 2 * NX>(own, nxt, xw);
-#pragma unroll
-    for (int i = 0; i < NX; ++i) {
-      ln[i] = nxt[i];
-      xn[i] = nxt[NX + i];
-    }
-    Model::derivs(ma, ctx, zz, ln, fs, xf, qv, A, Bm, gq, Hs);
-    const double m = hasU ? 1.0 : 0.0;
-    qv *= m;
-    if constexpr (!Model::kTableHess)
-#pragma unroll
-      for (int i = 0; i < NH; ++i) Hs[i] *= m;
-#pragma unroll
-    for (int i = 0; i < NZ; ++i) gq[i] *= m;
-#pragma unroll
-    for (int i = 0; i < NX; ++i) {
-      cdef[i] = hasU ? xf[i] - xn[i] : 0.0;
-      c0[i] = (valid && k == 0) ? x0[i] - zz[i] : 0.0;
-    }
-  };
-  // fresh: xf .. c0 hold the evaluation at the current (z, lam) (group-uniform)
-  bool fresh = false;
-  auto sweep = [&]() __attribute__((always_inline)) {
-    eval_at(z, lam);
-    fresh = true;
-  };
-
-  double mu = warm ? a.mu_init : 0.1, tau = fmax(kTauMin, 1.0 - mu);
-  const double mu_min = a.tol / 10.0;
-  double theta_max = 0.0, theta_min = 0.0;  // set at the first iterate
-  double dw_last = 0.0;
-  double fth = 0, fph = 0;  // filter entry #k of my instance (a ring of G entries in the lanes)
-  int nfilt = 0, fnext = 0;
-  // IPOPT's filter-reset heuristic: iterations in a row whose last rejected trial point was
-  // rejected by the filter alone, and resets so far in this solve
-  int frej = 0, nfreset = 0;
-  int status = valid ? 2 : 0;
-  bool done = !valid;
-  int it = 0;        // iteration of this instance's current solve
-  int its = 0;       // its iteration count when it finished
-  const int K = a.steps > 1 ? a.steps : 1;
-  int step = valid ? 0 : K - 1;  // closed-loop step of this instance (multi-step launches)
-  // every per-lane array is defined on every lane (lanes past node N included): no
-  // indeterminate values for the optimiser to exploit
-  double dz[NZ] = {}, dlam[NX] = {}, dzL[NZ] = {}, dzU[NZ] = {};
-  double Pk[NP] = {}, pk[NX] = {}, Kk[NU * NX] = {}, kfk[NU] = {};
-
-#ifdef MPCX_STAMPS
-  // 0 regularised iterations, 1 extra factorisations, 2 backtracks, 3 barrier updates,
-  // 4 fraction-to-boundary-limited steps (alpha_max < 1), 5 tiny steps, 6 filter rejections,
-  // 7 f-type (Armijo) acceptances, 8 factorisations by the sequential fallback of the scan,
-  // 9 filter resets, 10 first trials rejected with increased infeasibility (SOC-eligible),
-  // 11 accepted second-order corrections
-  int diag[kDiag] = {};
-  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long st_last = 0;
-  int st_ph = 9;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
-#endif
-  // ---- multi-step launches: the closed-loop step boundary of an instance that finished a
-  //      non-final step -- record it, plant x0 <- F(x0, u0*) on lane 0, shift primal and
-  //      multipliers one node (Casadi/multiple_shooting_casadi.py:271-287, the same values
-  //      the fused epilogue below writes), load the next step's references and schedule,
-  //      and restart the solve exactly as a new launch would from those buffers.
-  auto step_boundary = [&]() __attribute__((always_inline)) {
-    const bool bnd = done && step < K - 1;  // group-uniform
-    if (!__any(bnd)) return;
-    constexpr int NS = NZ + NX + NZ;
-    double own[NS], nxt[NS];
-#pragma unroll
-    for (int i = 0; i < NZ; ++i) {
-      own[i] = z[i];
-      own[NZ + NX + i] = (zU[i] - zL[i]) / fs;
-    }
-#pragma unroll
-    for (int i = 0; i < NX; ++i) own[NZ + i] = lam[i] / fs;
-    group_next<G, NS>(own, nxt, xw);
-    if (bnd) {
-      if (k == 0) {
-        if (a.status) a.status[(size_t)step * a.B + inst] = status;
-        if (a.iters) a.iters[(size_t)step * a.B + inst] = its;
-        double zp[NZ], xfp[NX], qp;
-#pragma unroll
-        for (int i = 0; i < NX; ++i) zp[i] = x0[i];
-#pragma unroll
-        for (int i = 0; i < NU; ++i) zp[NX + i] = z[NX + i];
-        Model::value(ma, ctx, zp, xfp, qp);
-#pragma unroll
-        for (int i = 0; i < NX; ++i) x0[i] = xfp[i];
-      }
-      ++step;
-      const double* Pn = a.Pseq ? a.Pseq + ((size_t)step * a.B + inst) * a.p_stride : Pin;
-      ModelArgs mst = ma;
-      if (a.tabseq) {
-        mst.lin.tab = a.tabseq + (size_t)step * a.B * N;
-        mst.lin.per_instance = 1;
-      }
-      Model::load_ctx(mst, inst, Pn, k, hasU, ctx);
-      const bool lastX = (k == N), lastU = (k == N - 1);
-      warm = a.warm_next != 0;
-#pragma unroll
-      for (int i = 0; i < NX; ++i) {
-        z[i] = hasX ? (lastX ? own[i] : nxt[i]) : 0.0;
-        lam[i] = (warm && hasX) ? (lastX ? own[NZ + i] : nxt[NZ + i]) : 0.0;
-        lx0[i] = (warm && hasX && k > 0) ? (lastX ? own[NZ + NX + i] : nxt[NZ + NX + i]) : 0.0;
-      }
-#pragma unroll
-      for (int i = 0; i < NU; ++i) {
-        z[NX + i] = hasU ? (lastU ? own[NX + i] : nxt[NX + i]) : 0.0;
-        lx0[NX + i] = (warm && hasU) ? (lastU ? own[NZ + 2 * NX + i] : nxt[NZ + 2 * NX + i]) : 0.0;
-      }
-      init_point();
-      fresh = false;
-      mu = warm ? a.mu_init : 0.1;
-      tau = fmax(kTauMin, 1.0 - mu);
-      fs = 1.0;
-      theta_max = theta_min = 0.0;
-      dw_last = 0.0;
-      nfilt = fnext = 0;
-      frej = nfreset = 0;
-      status = 2;
-      done = false;
-      it = 0;
-      its = 0;
-    }
-  };
-
-  // every pass is one IPM iteration for the instances still solving; instances that
-  // finished a step of a multi-step launch restart at the top of the next pass.  Bounded:
-  // each step ends after at most max_iter + 1 passes.
-  const long max_pass = (long)K * (a.max_iter + 2);
-  for (long pass = 0; pass <= max_pass; ++pass, ++it) {
-    if (K > 1) step_boundary();
-    // ------------------------------------------------------------ evaluation
-    //  skipped when the line search already evaluated the accepted point; only the groups
-    //  that need it evaluate (exec-masked, group-uniform), so an instance's sequence of
-    //  evaluation sites -- and its bits -- never depends on its wave neighbours
-    //  (models without kEvalInSearch evaluate unconditionally: nothing then stays live
-    //  across the back-edge)
-    if constexpr (Model::kEvalInSearch) {
-      if (__any(!fresh && !done))
-        if (!fresh) sweep();
-    } else {
-      sweep();
-    }
-    if (it == 0) {
-      // objective scaling (IPOPT nlp_scaling_method = gradient-based, max_gradient = 100).
-      // With lambda scaled by the same factor the Lagrangian's gradient and Hessian scale
-      // exactly by fs, so no re-evaluation is needed.
-      double gm = 0;
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) gm = fmax(gm, fabs(gq[i]));
-#ifdef MPCX_DEBUG_PRINT
-      const double gm_local = gm;
-#endif
-      gm = gmax<G>(gm, xw);
-#ifdef MPCX_DEBUG_PRINT
-      if (inst == 0 && (k % 32) == 0)
-        printf("k=%d wave=%d gm_local=%g gm=%g slot=%d nbound=%g lds=%p\n", k, (int)(threadIdx.x >> 6), gm_local, gm,
-               xw.slot, nbound, (void*)xw.buf);
-#endif
-      fs = gm > 100.0 ? 100.0 / gm : 1.0;
-      if constexpr (kDec) {
-        const bool d = !hasX || (xfree && (k == N || ctx.dec));
-        kb = (int)gmax<G>(d ? -1.0 : (double)k, xw) + 1;
-        pcv = false;
-      }
-      if (fs != 1.0) {  // group-uniform; given multipliers belong to the unscaled problem
-#pragma unroll
-        for (int i = 0; i < NX; ++i) lam[i] *= fs;
-#pragma unroll
-        for (int i = 0; i < NZ; ++i) gq[i] *= fs;
-        if constexpr (!Model::kTableHess)
-#pragma unroll
-          for (int i = 0; i < NH; ++i) Hs[i] *= fs;
-        if (warm)
-#pragma unroll
-          for (int i = 0; i < NZ; ++i) {
-            if (hL[i]) zL[i] = fmax(zL[i] * fs, a.mult_push);
-            if (hU[i]) zU[i] = fmax(zU[i] * fs, a.mult_push);
-          }
-      }
-      double theta0 = 0;
-#pragma unroll
-      for (int i = 0; i < NX; ++i) theta0 += fabs(cdef[i]) + fabs(c0[i]);
-      theta0 = gsum<G>(theta0, xw);
-      theta_max = 1e4 * fmax(1.0, theta0);
-      theta_min = 1e-4 * fmax(1.0, theta0);
-    }
-    STAMP(0);
-    // ------------------------------------------------------------ optimality error
-    double ln[NX];
-    group_next<G, NX>(lam, ln, xw);
-    double Ed = 0, Ecomp0 = 0, Ec = 0, lam1 = 0, z1 = 0;
-    double rd[NZ];
-#pragma unroll
-    for (int i = 0; i < NZ; ++i) rd[i] = 0;
-    if (hasX) {
-#pragma unroll
-      for (int i = 0; i < NX; ++i) rd[i] = gq[i] - lam[i];
-      if (hasU) {
-#pragma unroll
-        for (int j = 0; j < NX; ++j)
-#pragma unroll
-          for (int m = 0; m < NX; ++m)
-            if (Model::AMASK & (1ull << (m * NX + j))) rd[j] = fma(Model::jacA(ctx, A)[m * NX + j], ln[m], rd[j]);
-#pragma unroll
-        for (int l = 0; l < NU; ++l) {
-          double acc = gq[NX + l];
-#pragma unroll
-          for (int m = 0; m < NX; ++m)
-            if (Model::BMASK & (1ull << (m * NU + l))) acc = fma(Model::jacB(ctx, Bm)[m * NU + l], ln[m], acc);
-          rd[NX + l] = acc;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < NX; ++i) lam1 += fabs(lam[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < NZ; ++i) {
-      rd[i] += zU[i] - zL[i];
-      Ed = fmax(Ed, fabs(rd[i]));
-      z1 += zL[i] + zU[i];
-      if (hL[i]) Ecomp0 = fmax(Ecomp0, fabs((z[i] - lb[i]) * zL[i]));
-      if (hU[i]) Ecomp0 = fmax(Ecomp0, fabs((ub[i] - z[i]) * zU[i]));
-    }
-#pragma unroll
-    for (int i = 0; i < NX; ++i) Ec = fmax(Ec, fmax(fabs(cdef[i]), fabs(c0[i])));
-    Ed = gmax<G>(Ed, xw);
-    Ec = gmax<G>(Ec, xw);
-    Ecomp0 = gmax<G>(Ecomp0, xw);
-    lam1 = gsum<G>(lam1, xw);
-    z1 = gsum<G>(z1, xw);
-    const double sd = fmax(kSmax, (lam1 + z1) / (double)(ng + nw)) / kSmax;
-    const double sc = fmax(kSmax, nbound > 0 ? z1 / nbound : 0.0) / kSmax;
-    const double E0 = fmax(fmax(Ed / sd, Ec), Ecomp0 / sc);
-    if (!done && E0 <= a.tol) {
-      done = true;
-      status = 0;
-      its = it;
-    }
-    if (!done && it >= a.max_iter) {
-      done = true;
-      status = 2;
-      its = a.max_iter;
-    }
-#ifdef MPCX_DEBUG_PRINT
-    if (inst == 0 && (k % 64) == 0)
-      printf("OPT it=%d k=%d fs=%g Ed=%g Ec=%g E0=%g sd=%g lam1=%g z1=%g\n", it, k, fs, Ed, Ec, E0, sd, lam1, z1);
-#endif
-    if (__all(done && step == K - 1)) break;
-    // multi-step launches: a wave whose instances all just finished a step skips the rest of
-    // this pass (its Newton step would be discarded) and restarts at the step boundary
-    if (K > 1 && __all(done)) continue;
-
-    STAMP(1);
-    // ------------------------------------------------------------ barrier update
-    for (int rep = 0; rep < 32; ++rep) {
-      double Ecm = 0;
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) {
-        if (hL[i]) Ecm = fmax(Ecm, fabs((z[i] - lb[i]) * zL[i] - mu));
-        if (hU[i]) Ecm = fmax(Ecm, fabs((ub[i] - z[i]) * zU[i] - mu));
-      }
-      Ecm = gmax<G>(Ecm, xw);
-      const double Emu = fmax(fmax(Ed / sd, Ec), Ecm / sc);
-      const bool dec = !done && Emu <= kKappaEps * mu && mu > mu_min;
-      if (dec && !done) DIAG(3);
-      if (dec) {
-        static_assert(kThetaMu == 1.5, "mu^theta_mu evaluated as mu * sqrt(mu)");
-        mu = fmax(mu_min, fmin(kKappaMu * mu, mu * sqrt(mu)));
-        tau = fmax(kTauMin, 1.0 - mu);
-        nfilt = 0;
-        fnext = 0;
-      }
-      if (!__any(dec && it == 0)) break;
-    }
-
-    STAMP(2);
-    // ------------------------------------------------------------ barrier gradient, Sigma
-    double sig[NZ], gp[NZ];
-#pragma unroll
-    for (int i = 0; i < NZ; ++i) {
-      sig[i] = 0;
-      gp[i] = gq[i];
-      // one rcp64 per slack instead of IEEE divisions (each a ~10-instruction sequence)
-      if (hL[i]) {
-        const double rs = rcp64(z[i] - lb[i]);
-        sig[i] = fma(zL[i], rs, sig[i]);
-        gp[i] = fma(-mu, rs, gp[i]);
-      }
-      if (hU[i]) {
-        const double rs = rcp64(ub[i] - z[i]);
-        sig[i] = fma(zU[i], rs, sig[i]);
-        gp[i] = fma(mu, rs, gp[i]);
-      }
-    }
-
-    STAMP(3);
-    // ------------------------------------------------------------ Riccati + inertia correction
-    double delta = 0.0;
-    bool need = !done;  // instance still needs a factorisation
-    bool failed = false;
-    bool first = true;
-    Fac<NX, NU> fac = {};
-    for (int attempt = 0; attempt < 64; ++attempt) {
-      if (!__any(need)) break;
-      // node-parallel: stage Hessian + Sigma + delta (off the sequential path)
-      double Hd[NH];
-      // stage Hessian (table-Hessian models: 2 fs W of the stage table; none at node N)
-      const double hsc = Model::kTableHess ? (hasU ? 2.0 * fs : 0.0) : 1.0;
-      const double* Hsrc = Model::hessW(ctx, Hs);
-      const double* Aop = Model::jacA(ctx, A);
-      const double* Bop = Model::jacB(ctx, Bm);
-#pragma unroll
-      for (int i = 0; i < NH; ++i) Hd[i] = Model::kTableHess ? hsc * Hsrc[i] : Hsrc[i];
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) Hd[symix(i, i, NZ)] += sig[i] + delta;
-
-      // backward sweep: node N .. 0 (value function moves lane k+1 -> k)
-      double P[NP], p[NX];
-      bool okl = true;
-      bool seq = true;  // group-uniform: this instance needs the sequential recursion
-      if constexpr (Model::kParallelRiccati) {
-        // ---- log-depth associative scan of conditional value functions (pscan.h)
-        RElem<NX> e;
-        bool eok = true;
-        if (hasU) {
-          eok = relem_stage<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, Aop, Bop, cdef, e);
-        } else {
-          relem_identity<NX>(e);
-          if (hasX) {  // node N: terminal (0, 0, 0, Sigma_x + delta, barrier gradient)
-#pragma unroll
-            for (int i = 0; i < NX * NX; ++i) e.A[i] = 0.0;
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-#pragma unroll
-              for (int j = i; j < NX; ++j) e.J[symix(i, j, NX)] = (i == j) ? sig[i] + delta : 0.0;
-              e.p[i] = gp[i];
-            }
-          }
-        }
-        // Hillis-Steele suffix scan over the whole group through the LDS buffer `sbuf`
-        // (partner = thread t + d; block-uniform trip count, two barriers per level)
-        const int t = (int)threadIdx.x;
-        for (int d = 1; d < G && d <= N; d <<= 1) {
-          relem_store<NX>(e, sbuf, kSBS, t);
-          __syncthreads();
-          if (k + d < G) relem_combine_lds<NX>(e, sbuf + t + d, kSBS);
-          __syncthreads();
-        }
-        // value function of node k+1, then ONE node-parallel Riccati step per lane: gains,
-        // inertia test and (P_k, p_k) as the sequential recursion would produce them
-        double Jn[NP + NX], nx_[NP + NX];
-#pragma unroll
-        for (int i = 0; i < NP; ++i) Jn[i] = e.J[i];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) Jn[NP + i] = e.p[i];
-        group_next<G, NP + NX>(Jn, nx_, xw);
-        const double dl = (k == N) ? 1.0 : 0.0;
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-#pragma unroll
-          for (int j = i; j < NX; ++j) P[symix(i, j, NX)] = (i == j) ? dl * (sig[i] + delta) : 0.0;
-          p[i] = dl * gp[i];
-        }
-        double dev = 0.0, mag = 1.0;
-        if (hasU) {
-          okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, Aop, Bop, cdef, nx_, nx_ + NP, P, p, fac);
-#pragma unroll
-          for (int i = 0; i < NP; ++i) {
-            dev = fmax(dev, fabs(P[i] - e.J[i]));
-            mag = fmax(mag, fabs(P[i]));
-          }
-#pragma unroll
-          for (int i = 0; i < NX; ++i) {
-            dev = fmax(dev, fabs(p[i] - e.p[i]));
-            mag = fmax(mag, fabs(p[i]));
-          }
-        }
-        // scan usable: stage R positive definite, finite, and consistent with the step
-        const bool good = eok && dev <= 1e-8 * mag;  // false for NaN
-        seq = gmin<G>(good ? 1.0 : 0.0, xw) < 0.5;
-        DIAG_IF(seq && !done, 8);
-      }
-      if (__any(seq)) {  // sequential recursion (models without the scan, or its fallback)
-        if (seq) {
-          okl = true;
-          const double dl = (k == N) ? 1.0 : 0.0;  // P_N = Sigma_x + delta, p_N = barrier gradient
-#pragma unroll
-          for (int i = 0; i < NX; ++i) {
-#pragma unroll
-            for (int j = i; j < NX; ++j) P[symix(i, j, NX)] = (i == j) ? dl * (sig[i] + delta) : 0.0;
-            p[i] = dl * gp[i];
-          }
-        }
-        // decoupled suffix: with P_{k+1} reused, s = P_{k+1} c + p_{k+1} needs only p on the
-        // chain; P_{k+1} c comes from the stored Pk of node k+1, off the chain
-        const bool reuse = kDec && pcv && delta == 0.0;  // group-uniform
-        double vpc[kDec ? NX : 1];
-        bool okd = true;
-        if constexpr (kDec) {
-          double Pn1[NP];
-          group_next<G, NP>(Pk, Pn1, xw);
-#pragma unroll
-          for (int i = 0; i < NX; ++i) vpc[i] = riccati_pc_row<NX>(Pn1, cdef, i);
-          // reused stages: factors and P_k set here, off the chain (dec_prefactor)
-          if (reuse && k >= kb && k < N) {
-            okd = dec_prefactor<NX, NU>(Hd, fac);
-#pragma unroll
-            for (int i = 0; i < NP; ++i) P[i] = Pk[i];
-          }
-        }
-        if constexpr (G <= 64) {
-          for (int j = N - 1; j >= 0; --j) {
-            const bool cheap = reuse && j >= kb;
-            double Pin_[NP], pin_[NX];
-            if (!kDec || __any(!cheap)) {
-#pragma unroll
-              for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
-            if (seq && k == j) {
-              if (cheap) {  // group-uniform
-                dec_vector_step<NX, NU, Model::AMASK, Model::BMASK>(gp, Aop, Bop, vpc, pin_, p, fac);
-                okl = okd;
-              }
-              else
-                okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p,
-                                                                                     fac);
-            }
-          }
-        } else {  // wave by wave, N-side first; the value function crosses waves through LDS
-          const int wv = (int)(threadIdx.x >> 6);
-          for (int ph = XWave<G>::W - 1; ph >= 0; --ph) {
-            if (wv == ph) {
-              const double* in = xw.prev();  // (P, p) of node 64 (ph + 1), written last phase
-              const int jtop = 64 * ph + 63;
-              for (int j = min(N - 1, jtop); j >= 64 * ph; --j) {
-                const bool cheap = reuse && j >= kb;
-                double Pin_[NP], pin_[NX];
-                if (!kDec || __any(!cheap)) {
-#pragma unroll
-                  for (int i = 0; i < NP; ++i) Pin_[i] = from_next(P[i]);
-                }
-#pragma unroll
-                for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
-                if (j == jtop && lane == 63) {
-#pragma unroll
-                  for (int i = 0; i < NP; ++i) Pin_[i] = in[i];
-#pragma unroll
-                  for (int i = 0; i < NX; ++i) pin_[i] = in[NP + i];
-                }
-                if (seq && k == j) {
-                  if (cheap) {  // group-uniform
-                    dec_vector_step<NX, NU, Model::AMASK, Model::BMASK>(gp, Aop, Bop, vpc, pin_, p, fac);
-                    okl = okd;
-                  }
-                  else
-                    okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p,
-                                                                                         fac);
-                }
-              }
-              if (ph > 0 && lane == 0) {
-                double* out = xw.cur();
-#pragma unroll
-                for (int i = 0; i < NP; ++i) out[i] = P[i];
-#pragma unroll
-                for (int i = 0; i < NX; ++i) out[NP + i] = p[i];
-              }
-            }
-            xw.sync();
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < NP; ++i) Pk[i] = P[i];
-#pragma unroll
-      for (int i = 0; i < NX; ++i) pk[i] = p[i];
-      const bool ok = gmin<G>(okl ? 1.0 : 0.0, xw) > 0.5;
-      // IPOPT inertia correction (Algorithm IC)
-      if (need) {
-        if (ok) {
-          need = false;
-          if (delta > 0.0) dw_last = delta;
-          if (delta > 0.0) DIAG(0);
-        } else {
-          DIAG(1);
-          if (first) delta = dw_last == 0.0 ? kDw0 : fmax(kDwMin, kKwMinus * dw_last);
-          else delta *= dw_last == 0.0 ? kKwPlusBar : kKwPlus;
-          first = false;
-          if (delta > kDwMax) {
-            need = false;
-            failed = true;
-          }
-        }
-      }
-    }
-    if (!done && failed) {
-      done = true;
-      status = 3;
-      its = it;
-    }
-    if constexpr (kDec) pcv = !failed && delta == 0.0;  // Pk now holds a delta = 0 factorisation
-    riccati_gains<NX, NU>(fac, Kk, kfk);  // all lanes at once
-
-    STAMP(4);
-    // ------------------------------------------------------------ forward sweep: dw (lane k-1 -> k)
-    // (a lambda: the second-order correction re-runs it with other right-hand sides)
-    auto forward = [&](const double* cc_, const double* kf_, const double* pv_, const double* c0v_, double* dzo_,
-                       double* dlo_) __attribute__((always_inline)) {
-      // closed-loop map of the step, node-parallel (off the sequential chain):
-      // dx_{k+1} = (A + B K) dx_k + (c + B k_f);  du_k = k_f + K dx_k afterwards
-      double Acl[NX * NX], ccl[NX];
-#pragma unroll
-      for (int r = 0; r < NX; ++r) {
-        double acc = cc_[r];
-#pragma unroll
-        for (int l = 0; l < NU; ++l)
-          if (Model::BMASK & (1ull << (r * NU + l))) acc = fma(Model::jacB(ctx, Bm)[r * NU + l], kf_[l], acc);
-        ccl[r] = acc;
-#pragma unroll
-        for (int m = 0; m < NX; ++m) {
-          double e = (Model::AMASK & (1ull << (r * NX + m))) ? Model::jacA(ctx, A)[r * NX + m] : 0.0;
-#pragma unroll
-          for (int l = 0; l < NU; ++l)
-            if (Model::BMASK & (1ull << (r * NU + l))) e = fma(Model::jacB(ctx, Bm)[r * NU + l], Kk[l * NX + m], e);
-          Acl[r * NX + m] = e;
-        }
-      }
-      {
-        // dx_k = T_{k-1}( ... T_0(c0)) with affine T_j(x) = Acl_j x + ccl_j: an inclusive
-        // parallel prefix of map compositions (Hillis-Steele, log2 64 levels per wave, all
-        // lanes busy) instead of N+1 dependent steps.  Lane k starts with T_{k-1} (lane 0:
-        // the constant map c0) and composes with the partial map of lane k-d at each level.
-        // Multi-wave groups scan every wave at once; the first lane of wave w gets
-        // T_{64w-1} from wave w-1 through LDS, and the waves' partial results are chained
-        // by one LDS handoff of dx per wave boundary.
-        constexpr int NM = NX * NX + NX;
-        constexpr int GW = G < 64 ? G : 64;  // lanes scanned per wave
-        const int wv = G > 64 ? (int)(threadIdx.x >> 6) : 0;
-        double Am[NX * NX], cm[NX];
-        {
-          double own[NM], prv[NM];
-#pragma unroll
-          for (int i = 0; i < NX * NX; ++i) own[i] = Acl[i];
-#pragma unroll
-          for (int i = 0; i < NX; ++i) own[NX * NX + i] = ccl[i];
-#pragma unroll
-          for (int i = 0; i < NM; ++i) prv[i] = from_prev(own[i]);
-          if constexpr (G > 64) {  // lane 0 of wave w > 0: T_{64w-1} lives on lane 63 of wave w-1
-            double* b = xw.cur();
-            if (lane == 63 && wv < XWave<G>::W - 1)
-#pragma unroll
-              for (int i = 0; i < NM; ++i) b[wv * kXchStride + i] = own[i];
-            xw.sync();
-            if (lane == 0 && wv > 0)
-#pragma unroll
-              for (int i = 0; i < NM; ++i) prv[i] = xw.prev()[(wv - 1) * kXchStride + i];
-          }
-#pragma unroll
-          for (int i = 0; i < NX * NX; ++i) Am[i] = (k == 0) ? 0.0 : prv[i];
-#pragma unroll
-          for (int i = 0; i < NX; ++i) cm[i] = (k == 0) ? c0v_[i] : prv[NX * NX + i];
-        }
-        const int kw = k & (GW - 1);  // position inside the wave
-#pragma unroll
-        for (int d = 1; d < GW; d <<= 1) {
-          const int src = (lane - d) & 63;
-          double Ao[NX * NX], co[NX];
-#pragma unroll
-          for (int i = 0; i < NX * NX; ++i) Ao[i] = from_lane(Am[i], src);
-#pragma unroll
-          for (int i = 0; i < NX; ++i) co[i] = from_lane(cm[i], src);
-          if (kw >= d) {  // compose: (Am, cm) o (Ao, co)
-            double An[NX * NX], cn[NX];
-#pragma unroll
-            for (int r = 0; r < NX; ++r) {
-              double acc = cm[r];
-#pragma unroll
-              for (int m = 0; m < NX; ++m) acc = fma(Am[r * NX + m], co[m], acc);
-              cn[r] = acc;
-#pragma unroll
-              for (int c = 0; c < NX; ++c) {
-                double e = Am[r * NX] * Ao[c];
-#pragma unroll
-                for (int m = 1; m < NX; ++m) e = fma(Am[r * NX + m], Ao[m * NX + c], e);
-                An[r * NX + c] = e;
-              }
-            }
-#pragma unroll
-            for (int i = 0; i < NX * NX; ++i) Am[i] = An[i];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) cm[i] = cn[i];
-          }
-        }
-        if constexpr (G > 64) {
-          // wave w's lanes hold maps dx_{64w-1} -> dx_k; chain the waves in order
-          for (int ph = 1; ph < XWave<G>::W; ++ph) {
-            double* b = xw.cur();
-            if (wv == ph - 1 && lane == 63)
-#pragma unroll
-              for (int i = 0; i < NX; ++i) b[i] = cm[i];
-            xw.sync();
-            if (wv == ph) {
-              const double* in = xw.prev();
-              double cn[NX];
-#pragma unroll
-              for (int r = 0; r < NX; ++r) {
-                double acc = cm[r];
-#pragma unroll
-                for (int m = 0; m < NX; ++m) acc = fma(Am[r * NX + m], in[m], acc);
-                cn[r] = acc;
-              }
-#pragma unroll
-              for (int i = 0; i < NX; ++i) cm[i] = cn[i];
-            }
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dzo_[i] = cm[i];
-      }
-      // du_k = k_f + K dx_k on all lanes at once (the last node has no control)
-#pragma unroll
-      for (int l = 0; l < NU; ++l) {
-        double acc = kf_[l];
-#pragma unroll
-        for (int m = 0; m < NX; ++m) acc = fma(Kk[l * NX + m], dzo_[m], acc);
-        dzo_[NX + l] = (k < N) ? acc : 0.0;
-      }
-      // lambda+ = P_k dx_k + p_k (node-parallel, after the sequential sweep)
-#pragma unroll
-      for (int i = 0; i < NX; ++i) {
-        double acc = pv_[i];
-#pragma unroll
-        for (int m = 0; m < NX; ++m) acc = fma(Pk[symix(i, m, NX)], dzo_[m], acc);
-        dlo_[i] = acc - lam[i];
-      }
-      if (!hasX) {
-#pragma unroll
-        for (int i = 0; i < NZ; ++i) dzo_[i] = 0.0;
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dlo_[i] = 0.0;
-      }
-    };
-    forward(cdef, kfk, pk, c0, dz, dlam);
-
-    STAMP(5);
-    // ------------------------------------------------------------ bound-dual step, fraction to boundary
-    double amax_l = 1.0, az_l = 1.0, tiny_l = 0.0, gd_l = 0.0;
-#pragma unroll
-    for (int i = 0; i < NZ; ++i) {
-      dzL[i] = dzU[i] = 0.0;
-      const double rdz = rcp64(dz[i]);
-      if (hL[i]) {
-        const double s = z[i] - lb[i], rs = rcp64(s);
-        dzL[i] = fma(mu, rs, -zL[i]) - zL[i] * rs * dz[i];
-        if (dz[i] < 0) amax_l = fmin(amax_l, -tau * s * rdz);
-        if (dzL[i] < 0) az_l = fmin(az_l, -tau * zL[i] * rcp64(dzL[i]));
-      }
-      if (hU[i]) {
-        const double s = ub[i] - z[i], rs = rcp64(s);
-        dzU[i] = fma(mu, rs, -zU[i]) + zU[i] * rs * dz[i];
-        if (dz[i] > 0) amax_l = fmin(amax_l, tau * s * rdz);
-        if (dzU[i] < 0) az_l = fmin(az_l, -tau * zU[i] * rcp64(dzU[i]));
-      }
-      const bool own = (i < NX) ? hasX : hasU;
-      if (own) {
-        tiny_l = fmax(tiny_l, fabs(dz[i]) * rcp64(1.0 + fabs(z[i])));
-        gd_l += gp[i] * dz[i];
-      }
-    }
-    const double amax = gmin<G>(amax_l, xw), tiny = gmax<G>(tiny_l, xw);
-    double az = gmin<G>(az_l, xw);  // dual step length (a second-order correction replaces it)
-    if (!done && amax < 1.0) DIAG(4);
-    if (!done && tiny < 10.0 * kEps) DIAG(5);
-    const double gd = gsum<G>(gd_l, xw);
-
-    STAMP(6);
-    // ------------------------------------------------------------ filter line search
-    double thk_l = 0, phk_l = (hasU ? fs * qv : 0.0) - mu * barrier_logsum<NZ>(z, lb, ub, hL, hU);
-#pragma unroll
-    for (int i = 0; i < NX; ++i) thk_l += fabs(cdef[i]) + fabs(c0[i]);
-    const double thk = gsum<G>(thk_l, xw), phk = gsum<G>(phk_l, xw);
-    const bool tinystep = tiny < 10.0 * kEps;
-    double alpha = amax;
-    bool searching = !done && !tinystep;
-    bool accepted = !done && tinystep;
-    bool ftype = tinystep;
-    bool trial_fresh = false;  // accepted at the first trial, which evaluated derivatives
-    bool lastrej_f = false;    // the last rejected trial passed the sufficient decrease test but not the filter
-    // switching condition alpha (-gd)^s_phi > delta theta^s_theta  <=>  alpha > sw_a with
-    // sw_a = delta theta^s_theta / (-gd)^s_phi -- also the third term of alpha_min; one exp of
-    // logs, loop-invariant over the trials
-    const double sw_a = gd < 0 ? exp(log(kDeltaSw) + kSTheta * log(thk) - kSPhi * log(-gd)) : 0.0;
-    const double amin = gd < 0 ? kGammaAlpha * fmin(kGammaTheta, fmin(kGammaPhi * thk / (-gd), sw_a))
-                               : kGammaAlpha * kGammaTheta;
-    if constexpr (!Model::kSOC) {
-    for (int ls = 0; ls < 80; ++ls) {
-      if (!__any(searching)) break;
-      double zt[NZ];
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) zt[i] = fma(alpha, dz[i], z[i]);  // the update's exact expression
-      double tht_l = 0, pht_l = 0;
-      if (Model::kEvalInSearch && ls == 0) {
-        if (searching) {  // group-uniform (block-uniform for multi-wave groups)
-          double lt[NX];
-#pragma unroll
-          for (int i = 0; i < NX; ++i) lt[i] = fma(alpha, dlam[i], lam[i]);
-          eval_at(zt, lt);
-          fresh = false;  // until accepted
-#pragma unroll
-          for (int i = 0; i < NX; ++i) tht_l += fabs(cdef[i]) + fabs(c0[i]);
-          pht_l = fs * qv;  // masked to 0 without an interval
-        }
-      } else {
-        double xtn[NX];
-        group_next<G, NX>(zt, xtn, xw);
-        double xft[NX], qt;
-        Model::value(ma, ctx, zt, xft, qt);
-        if (hasU) {
-#pragma unroll
-          for (int i = 0; i < NX; ++i) tht_l += fabs(xft[i] - xtn[i]);
-          pht_l = fs * qt;
-        }
-        if (valid && k == 0)
-#pragma unroll
-          for (int i = 0; i < NX; ++i) tht_l += fabs(x0[i] - zt[i]);
-      }
-      pht_l -= mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU);
-      const double tht = gsum<G>(tht_l, xw), pht = gsum<G>(pht_l, xw);
-      const double inF = (k < nfilt && tht >= fth && pht >= fph) ? 1.0 : 0.0;
-      const bool infilter = gmax<G>(inF, xw) > 0.5;
-      if (searching) {
-        // sufficient decrease (switching condition + Armijo, or theta/phi decrease), then the
-        // filter -- IPOPT's order, which decides whether a rejection was the filter's
-        bool acc = isfinite(pht) && isfinite(tht) && tht <= theta_max;
-        bool ft = false;
-        if (acc) {
-          const bool sw = gd < 0 && alpha > sw_a;
-          if (thk <= theta_min && sw) {
-            acc = pht - phk <= kEtaPhi * alpha * gd + 10.0 * kEps * fabs(phk);
-            ft = acc;
-          } else {
-            acc = tht <= (1.0 - kGammaTheta) * thk || pht <= phk - kGammaPhi * thk + 10.0 * kEps * fabs(phk);
-          }
-        }
-        if (acc && infilter) {
-          acc = false;
-          lastrej_f = true;
-        } else if (!acc) {
-          lastrej_f = false;
-        }
-        if (searching && infilter) DIAG(6);
-        if (acc) {
-          searching = false;
-          accepted = true;
-          ftype = ft;
-          trial_fresh = Model::kEvalInSearch && ls == 0;
-          if (ft) DIAG(7);
-        } else {
-          DIAG(2);
-          alpha *= 0.5;
-          if (alpha < amin) searching = false;  // would need restoration
-        }
-      }
-    }
-    } else {  // models with the second-order correction (their trials evaluate values only)
-    // trial point zt: constraint violation, barrier objective, filter membership (group sums);
-    // ct / ct0 receive the trial's own constraint values (interval k, and g_0 on lane 0)
-    auto trial_value = [&](const double* zt, double& tht, double& pht, bool& infilter, double* ct, double* ct0)
-                           __attribute__((always_inline)) {
-      double xtn[NX];
-      group_next<G, NX>(zt, xtn, xw);
-      double xft[NX], qt;
-      Model::value(ma, ctx, zt, xft, qt);
-      double tht_l = 0, pht_l = 0;
-#pragma unroll
-      for (int i = 0; i < NX; ++i) {
-        ct[i] = hasU ? xft[i] - xtn[i] : 0.0;
-        ct0[i] = (valid && k == 0) ? x0[i] - zt[i] : 0.0;
-      }
-      if (hasU) {
-#pragma unroll
-        for (int i = 0; i < NX; ++i) tht_l += fabs(ct[i]);
-        pht_l = fs * qt;
-      }
-      if (valid && k == 0)
-#pragma unroll
-        for (int i = 0; i < NX; ++i) tht_l += fabs(ct0[i]);
-      pht_l -= mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU);
-      tht = gsum<G>(tht_l, xw);
-      pht = gsum<G>(pht_l, xw);
-      const double inF = (k < nfilt && tht >= fth && pht >= fph) ? 1.0 : 0.0;
-      infilter = gmax<G>(inF, xw) > 0.5;
-    };
-    // acceptance of a trial point for step length al (W&B 2006 A-5.4): sufficient decrease
-    // (switching condition + Armijo, or theta/phi decrease), then the filter -- IPOPT's order,
-    // which decides whether a rejection was the filter's
-    auto acceptable = [&](double tht, double pht, bool infilter, double al, bool& ft) __attribute__((always_inline)) {
-      bool acc = isfinite(pht) && isfinite(tht) && tht <= theta_max;
-      ft = false;
-      if (acc) {
-        const bool sw = gd < 0 && al > sw_a;
-        if (thk <= theta_min && sw) {
-          acc = pht - phk <= kEtaPhi * al * gd + 10.0 * kEps * fabs(phk);
-          ft = acc;
-        } else {
-          acc = tht <= (1.0 - kGammaTheta) * thk || pht <= phk - kGammaPhi * thk + 10.0 * kEps * fabs(phk);
-        }
-      }
-      if (acc && infilter) {
-        acc = false;
-        lastrej_f = true;
-      } else if (!acc) {
-        lastrej_f = false;
-      }
-      return acc;
-    };
-    for (int ls = 0; ls < 80; ++ls) {
-      if (!__any(searching)) break;
-      double zt[NZ];
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) zt[i] = fma(alpha, dz[i], z[i]);  // the update's exact expression
-      double tht, pht;
-      bool infilter;
-      double ct[NX], ct0[NX];  // constraint values at the trial point (value path)
-      trial_value(zt, tht, pht, infilter, ct, ct0);
-      bool soc_want = false;  // first trial rejected with more infeasibility: second-order correction
-      if (searching) {
-        bool ft;
-        const bool acc = acceptable(tht, pht, infilter, alpha, ft);
-        if (infilter) DIAG(6);
-        if (acc) {
-          searching = false;
-          accepted = true;
-          ftype = ft;
-          if (ft) DIAG(7);
-        } else {
-          DIAG(2);
-          DIAG_IF(ls == 0 && tht >= thk, 10);
-          soc_want = ls == 0 && tht >= thk;
-          if (!soc_want) {
-            alpha *= 0.5;
-            if (alpha < amin) searching = false;  // would need restoration
-          }
-        }
-      }
-      {
-        // IPOPT's second-order correction (W&B 2006 A-5.7-A-5.9, max_soc = 4, kappa_soc = 0.99):
-        // re-solve the Newton system (same factorisation) with the constraint residual
-        // c_soc = alpha c(x_k) + c(x_trial), step to the boundary along the correction, and
-        // test it with the first trial's step length; accumulate and retry while the
-        // infeasibility keeps shrinking by kappa_soc
-        if (ls == 0 && __any(soc_want)) {
-          bool son = soc_want;
-          double cs[NX], cs0[NX];
-#pragma unroll
-          for (int i = 0; i < NX; ++i) {
-            cs[i] = fma(alpha, cdef[i], ct[i]);
-            cs0[i] = fma(alpha, c0[i], ct0[i]);
-          }
-          double th_old = thk;
-          double Pn1[NP];  // P_{k+1}
-          group_next<G, NP>(Pk, Pn1, xw);
-          for (int ps = 0; ps < 4; ++ps) {
-            if (!__any(son)) break;
-            // backward recursion of the value function's linear part only (the factorisation
-            // P_k, K_k, Huu' is the current iteration's): p_k = gx + K^T gu with
-            // s = p_{k+1} + P_{k+1} c_soc, gx = gp_x + A^T s, gu = gp_u + B^T s; k_f = -Huu'^-1 gu
-            double pv[NX], kfs[NU];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) pv[i] = (k == N) ? gp[i] : 0.0;
-#pragma unroll
-            for (int l = 0; l < NU; ++l) kfs[l] = 0.0;
-            auto soc_step = [&](const double* pin) __attribute__((always_inline)) {
-              const double* Aop = Model::jacA(ctx, A);
-              const double* Bop = Model::jacB(ctx, Bm);
-              double sv[NX], gu[NU];
-#pragma unroll
-              for (int i = 0; i < NX; ++i) {
-                double acc = pin[i];
-#pragma unroll
-                for (int m = 0; m < NX; ++m) acc = fma(Pn1[symix(i, m, NX)], cs[m], acc);
-                sv[i] = acc;
-              }
-#pragma unroll
-              for (int l = 0; l < NU; ++l) {
-                double acc = gp[NX + l];
-#pragma unroll
-                for (int m = 0; m < NX; ++m)
-                  if (Model::BMASK & (1ull << (m * NU + l))) acc = fma(Bop[m * NU + l], sv[m], acc);
-                gu[l] = acc;
-              }
-#pragma unroll
-              for (int i = 0; i < NX; ++i) {
-                double acc = gp[i];
-#pragma unroll
-                for (int m = 0; m < NX; ++m)
-                  if (Model::AMASK & (1ull << (m * NX + i))) acc = fma(Aop[m * NX + i], sv[m], acc);
-#pragma unroll
-                for (int l = 0; l < NU; ++l) acc = fma(Kk[l * NX + i], gu[l], acc);
-                pv[i] = acc;
-              }
-              if constexpr (NU == 1) {
-                kfs[0] = -fac.r0 * gu[0];
-              } else {
-                const double z1 = fac.r1 * fma(-fac.t, gu[0], gu[1]);
-                kfs[1] = -z1;
-                kfs[0] = -fma(fac.r0, gu[0], -fac.t * z1);
-              }
-            };
-            if constexpr (G <= 64) {
-              for (int j = N - 1; j >= 0; --j) {
-                double pin[NX];
-#pragma unroll
-                for (int i = 0; i < NX; ++i) pin[i] = from_next(pv[i]);
-                if (k == j) soc_step(pin);
-              }
-            } else {  // wave by wave, N-side first; p crosses waves through LDS
-              const int wv = (int)(threadIdx.x >> 6);
-              for (int ph = XWave<G>::W - 1; ph >= 0; --ph) {
-                if (wv == ph) {
-                  const double* in = xw.prev();
-                  const int jtop = 64 * ph + 63;
-                  for (int j = min(N - 1, jtop); j >= 64 * ph; --j) {
-                    double pin[NX];
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) pin[i] = from_next(pv[i]);
-                    if (j == jtop && lane == 63)
-#pragma unroll
-                      for (int i = 0; i < NX; ++i) pin[i] = in[i];
-                    if (k == j) soc_step(pin);
-                  }
-                  if (ph > 0 && lane == 0) {
-                    double* out = xw.cur();
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) out[i] = pv[i];
-                  }
-                }
-                xw.sync();
-              }
-            }
-            double dzs[NZ], dls[NX];
-            forward(cs, kfs, pv, cs0, dzs, dls);
-            // primal and dual fraction to the boundary along the correction
-            double am_l = 1.0, azs_l = 1.0, dzLs[NZ], dzUs[NZ];
-#pragma unroll
-            for (int i = 0; i < NZ; ++i) {
-              dzLs[i] = dzUs[i] = 0.0;
-              const double rdz = rcp64(dzs[i]);
-              if (hL[i]) {
-                const double sl = z[i] - lb[i], rs = rcp64(sl);
-                dzLs[i] = fma(mu, rs, -zL[i]) - zL[i] * rs * dzs[i];
-                if (dzs[i] < 0) am_l = fmin(am_l, -tau * sl * rdz);
-                if (dzLs[i] < 0) azs_l = fmin(azs_l, -tau * zL[i] * rcp64(dzLs[i]));
-              }
-              if (hU[i]) {
-                const double su = ub[i] - z[i], rs = rcp64(su);
-                dzUs[i] = fma(mu, rs, -zU[i]) + zU[i] * rs * dzs[i];
-                if (dzs[i] > 0) am_l = fmin(am_l, tau * su * rdz);
-                if (dzUs[i] < 0) azs_l = fmin(azs_l, -tau * zU[i] * rcp64(dzUs[i]));
-              }
-            }
-            const double as = gmin<G>(am_l, xw), azs = gmin<G>(azs_l, xw);
-            double zs[NZ];
-#pragma unroll
-            for (int i = 0; i < NZ; ++i) zs[i] = fma(as, dzs[i], z[i]);
-            double ths, phs, cts[NX], cts0[NX];
-            bool infs;
-            trial_value(zs, ths, phs, infs, cts, cts0);
-#ifdef MPCX_DEBUG_PRINT
-            if (inst == 0 && k == 0)
-              printf("SOC it=%d ps=%d son=%d alpha0=%g as=%g thk=%.17g phk=%.17g ths=%.17g phs=%.17g infs=%d nfilt=%d\n", it,
-                     ps, (int)son, alpha, as, thk, phk, ths, phs, (int)infs, nfilt);
-#endif
-            if (son) {
-              bool ft;
-              if (acceptable(ths, phs, infs, alpha, ft)) {  // tested with the first trial's alpha
-                son = false;
-                searching = false;
-                accepted = true;
-                ftype = ft;
-                alpha = as;
-                az = azs;
-#pragma unroll
-                for (int i = 0; i < NZ; ++i) {
-                  dz[i] = dzs[i];
-                  dzL[i] = dzLs[i];
-                  dzU[i] = dzUs[i];
-                }
-#pragma unroll
-                for (int i = 0; i < NX; ++i) dlam[i] = dls[i];
-                DIAG(11);
-              } else if (ps == 3 || ths > 0.99 * th_old) {
-                son = false;
-              } else {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) {
-                  cs[i] = fma(as, cs[i], cts[i]);
-                  cs0[i] = fma(as, cs0[i], cts0[i]);
-                }
-                th_old = ths;
-              }
-            }
-          }
-          if (soc_want && searching) {  // correction failed: backtrack along the original direction
-            alpha *= 0.5;
-            if (alpha < amin) searching = false;
-          }
-        }
-      }
-    }
-    }
-    if (!done && !accepted) {
-      done = true;
-      status = 3;
-      its = it;
-    }
-
-    STAMP(7);
-    // ------------------------------------------------------------ update iterate
-    if (!done) {
-      if (!ftype) {  // augment the filter (entry slot fnext lives on lane fnext)
-        if (k == fnext) {
-          fth = (1.0 - kGammaTheta) * thk;
-          fph = phk - kGammaPhi * thk;
-        }
-        fnext = (fnext + 1) & (G - 1);
-        nfilt = nfilt < G ? nfilt + 1 : G;
-      }
-      // filter reset (IPOPT filter_reset_trigger = 5, max_filter_resets = 5): the filter is
-      // cleared once the last rejection of 5 successive iterations was the filter's
-      if (lastrej_f) {
-        if (++frej >= kFilterResetTrigger && nfreset < kMaxFilterResets) {
-          nfilt = fnext = 0;
-          ++nfreset;
-          frej = 0;
-          DIAG(9);
-        }
-      } else {
-        frej = 0;
-      }
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) z[i] = fma(alpha, dz[i], z[i]);
-#pragma unroll
-      for (int i = 0; i < NX; ++i) lam[i] = fma(alpha, dlam[i], lam[i]);
-      fresh = trial_fresh;
-#pragma unroll
-      for (int i = 0; i < NZ; ++i) {
-        if (hL[i]) {
-          const double mrs = mu * rcp64(z[i] - lb[i]);
-          zL[i] = fmax(fmin(zL[i] + az * dzL[i], kKappaSigma * mrs), mrs * (1.0 / kKappaSigma));
-        }
-        if (hU[i]) {
-          const double mrs = mu * rcp64(ub[i] - z[i]);
-          zU[i] = fmax(fmin(zU[i] + az * dzU[i], kKappaSigma * mrs), mrs * (1.0 / kKappaSigma));
-        }
-      }
-    }
-    STAMP(8);
-  }
-  STAMP(9);
-#ifdef MPCX_STAMPS
-  if (g_mpcx_diag && valid && k == 0)
-    for (int i = 0; i < kDiag; ++i) g_mpcx_diag[(size_t)inst * kDiag + i] = diag[i];
-  if (g_mpcx_stamps && (threadIdx.x & 63) == 0) {
-    const long wv = gid / 64;
-    for (int i = 0; i < 10; ++i) g_mpcx_stamps[wv * 10 + i] = st_acc[i];
-  }
-#endif
-
-  // ---- results (an instance that ended in a failed line search holds a trial's evaluation)
-  if constexpr (Model::kEvalInSearch) {
-    if (__any(!fresh))
-      if (!fresh) sweep();
-  }
-  const double fsum = gsum<G>(hasU ? qv : 0.0, xw);
-#ifdef MPCX_DEBUG_PRINT
-  if (inst == 0 && (k % 64) == 0)
-    printf("END k=%d fs=%g mu=%g it=%d lam0=%g z0=%g zL=%g zU=%g\n", k, fs, mu, it, lam[0], z[0], zL[NX], zU[NX]);
-#endif
-  if (valid) {
-    double* w = a.w_out + (size_t)inst * nw;
-    if (hasX)
-      for (int i = 0; i < NX; ++i) w[ixw<NX, NU>(k, i)] = z[i];
-    if (hasU)
-      for (int i = 0; i < NU; ++i) w[iuw<NX, NU>(k, i)] = z[NX + i];
-    if (a.lam_out && hasX)
-      for (int i = 0; i < NX; ++i) a.lam_out[(size_t)inst * ng + NX * k + i] = lam[i] / fs;
-    if (a.lamx_out) {
-      double* lx = a.lamx_out + (size_t)inst * nw;
-      if (hasX)
-        for (int i = 0; i < NX; ++i) lx[ixw<NX, NU>(k, i)] = (zU[i] - zL[i]) / fs;
-      if (hasU)
-        for (int i = 0; i < NU; ++i) lx[iuw<NX, NU>(k, i)] = (zU[NX + i] - zL[NX + i]) / fs;
-    }
-    if (k == 0) {
-      if (a.f_out) a.f_out[inst] = fsum;
-      if (a.status) a.status[(size_t)step * a.B + inst] = status;
-      if (a.iters) a.iters[(size_t)step * a.B + inst] = its;
-    }
-  }
-
-  // ---- fused receding-horizon update (Casadi/multiple_shooting_casadi.py:271-287), the
-  //      same result as shift_kernel: node k takes node k+1's primal and multipliers
-  //      (last node / interval repeated), x0 <- F(x0, u_0*) on lane 0.
-  if (a.w0_next) {  // kernel-uniform
-    constexpr int NS = NZ + NX + NZ;  // z, lam, lamx of the next node
-    double own[NS], nxt[NS];
-#pragma unroll
-    for (int i = 0; i < NZ; ++i) {
-      own[i] = z[i];
-      own[NZ + NX + i] = (zU[i] - zL[i]) / fs;
-    }
-#pragma unroll
-    for (int i = 0; i < NX; ++i) own[NZ + i] = lam[i] / fs;
-    group_next<G, NS>(own, nxt, xw);
-    if (valid) {
-      const bool lastX = (k == N), lastU = (k == N - 1);
-      double* w0n = a.w0_next + (size_t)inst * nw;
-      if (hasX)
-        for (int i = 0; i < NX; ++i) w0n[ixw<NX, NU>(k, i)] = lastX ? own[i] : nxt[i];
-      if (hasU)
-        for (int i = 0; i < NU; ++i) w0n[iuw<NX, NU>(k, i)] = lastU ? own[NX + i] : nxt[NX + i];
-      if (a.lam0_next && hasX)
-        for (int i = 0; i < NX; ++i) a.lam0_next[(size_t)inst * ng + NX * k + i] = lastX ? own[NZ + i] : nxt[NZ + i];
-      if (a.lamx0_next) {
-        double* lx = a.lamx0_next + (size_t)inst * nw;
-        if (hasX)
-          for (int i = 0; i < NX; ++i)
-            lx[ixw<NX, NU>(k, i)] = k == 0 ? 0.0 : (lastX ? own[NZ + NX + i] : nxt[NZ + NX + i]);
-        if (hasU)
-          for (int i = 0; i < NU; ++i)
-            lx[iuw<NX, NU>(k, i)] = lastU ? own[NZ + NX + NX + i] : nxt[NZ + NX + NX + i];
-      }
-      if (k == 0) {  // plant: x0 <- F(x0, u_0*) with the stage-0 model
-        double zp[NZ], xfp[NX], qp;
-#pragma unroll
-        for (int i = 0; i < NX; ++i) zp[i] = x0[i];
-#pragma unroll
-        for (int i = 0; i < NU; ++i) zp[NX + i] = z[NX + i];
-        Model::value(ma, ctx, zp, xfp, qp);
-        double* pn = a.P_next + (size_t)inst * a.p_stride;
-        for (int i = 0; i < NX; ++i) pn[i] = xfp[i];
-      }
-    }
-  }
-}
 
 // ------------------------------------------------------------------------------
 // RK4 + Jacobian sweep over B x N unicycle intervals, tiled structure of arrays.
@@ -1488,171 +80,6 @@ __global__ __launch_bounds__(256) void rk4_sens_kernel(int B, int N, StageParams
   }
 }
 
-// Plant: x+ = F(x0, u) (Casadi/multiple_shooting_casadi.py:273), one thread per instance.
-template <class Model>
-__global__ void plant_kernel(SolveArgs a, const double* __restrict__ U, double* __restrict__ XF,
-                             double* __restrict__ QF) {
-  constexpr int NX = Model::NX, NU = Model::NU;
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= a.B) return;
-  const double* p = a.P + (size_t)b * a.p_stride;
-  const ModelArgs ma = model_args(a);
-  typename Model::Ctx ctx;
-  Model::load_ctx(ma, b, p, 0, true, ctx);
-  double z[NX + NU], xf[NX], q;
-  for (int i = 0; i < NX; ++i) z[i] = p[i];
-  for (int i = 0; i < NU; ++i) z[NX + i] = U[(size_t)b * NU + i];
-  Model::value(ma, ctx, z, xf, q);
-  for (int i = 0; i < NX; ++i) XF[(size_t)b * NX + i] = xf[i];
-  if (QF) QF[b] = q;
-}
-
-// Closed-loop update (:271-287): x0 <- F(x0, u0*), w0_next = w shifted one interval;
-// multipliers shifted alike when given (warm start of the next solve).
-template <class Model>
-__global__ void shift_kernel(SolveArgs a, double* __restrict__ P, const double* __restrict__ W,
-                             double* __restrict__ W0, const double* __restrict__ L, double* __restrict__ L0,
-                             const double* __restrict__ LX, double* __restrict__ LX0) {
-  constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU;
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= a.B) return;
-  const int N = a.N, nw = NX + NZ * N, ng = NX * (N + 1);
-  double* p = P + (size_t)b * a.p_stride;
-  const double* w = W + (size_t)b * nw;
-  double* w0 = W0 + (size_t)b * nw;
-  const ModelArgs ma = model_args(a);
-  typename Model::Ctx ctx;
-  Model::load_ctx(ma, b, p, 0, true, ctx);
-  double z[NZ], xf[NX], q;
-  for (int i = 0; i < NX; ++i) z[i] = p[i];
-  for (int i = 0; i < NU; ++i) z[NX + i] = w[iuw<NX, NU>(0, i)];
-  Model::value(ma, ctx, z, xf, q);
-  for (int i = 0; i < NX; ++i) p[i] = xf[i];
-  // shifted guess: X_k <- X_{k+1}, U_k <- U_{k+1}; last node/interval repeated
-  for (int kk = 0; kk <= N; ++kk) {
-    const int src = kk < N ? kk + 1 : N;
-    for (int i = 0; i < NX; ++i) w0[ixw<NX, NU>(kk, i)] = w[ixw<NX, NU>(src, i)];
-    if (LX && LX0)
-      for (int i = 0; i < NX; ++i)
-        LX0[(size_t)b * nw + ixw<NX, NU>(kk, i)] = kk == 0 ? 0.0 : LX[(size_t)b * nw + ixw<NX, NU>(src, i)];
-    if (L && L0)
-      for (int i = 0; i < NX; ++i) L0[(size_t)b * ng + NX * kk + i] = L[(size_t)b * ng + NX * src + i];
-    if (kk < N) {
-      const int su = kk + 1 < N ? kk + 1 : N - 1;
-      for (int i = 0; i < NU; ++i) w0[iuw<NX, NU>(kk, i)] = w[iuw<NX, NU>(su, i)];
-      if (LX && LX0)
-        for (int i = 0; i < NU; ++i) LX0[(size_t)b * nw + iuw<NX, NU>(kk, i)] = LX[(size_t)b * nw + iuw<NX, NU>(su, i)];
-    }
-  }
-}
-
-// Constraint values g = [x0 - X_0; F(X_k, U_k) - X_{k+1}] (Casadi/multiple_shooting_casadi.py:131,172-175).
-template <class Model>
-__global__ void constraints_kernel(SolveArgs a, const double* __restrict__ W, double* __restrict__ Gout) {
-  constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU;
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= a.B) return;
-  const int N = a.N, nw = NX + NZ * N, ng = NX * (N + 1);
-  const double* p = a.P + (size_t)b * a.p_stride;
-  const double* w = W + (size_t)b * nw;
-  double* g = Gout + (size_t)b * ng;
-  for (int i = 0; i < NX; ++i) g[i] = p[i] - w[i];
-  const ModelArgs ma = model_args(a);
-  for (int kk = 0; kk < N; ++kk) {
-    typename Model::Ctx ctx;
-    Model::load_ctx(ma, b, p, kk, true, ctx);
-    double z[NZ], xf[NX], q;
-    for (int i = 0; i < NX; ++i) z[i] = w[ixw<NX, NU>(kk, i)];
-    for (int i = 0; i < NU; ++i) z[NX + i] = w[iuw<NX, NU>(kk, i)];
-    Model::value(ma, ctx, z, xf, q);
-    for (int i = 0; i < NX; ++i) g[NX * (kk + 1) + i] = xf[i] - w[ixw<NX, NU>(kk + 1, i)];
-  }
-}
-
-#ifdef MPCX_STAMPS
-extern "C" int mpcx_diag_set_stamp_buffer(void* d_buf) {
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_mpcx_stamps), &d_buf, sizeof(void*));
-}
-extern "C" int mpcx_diag_set_counter_buffer(void* d_buf) {
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_mpcx_diag), &d_buf, sizeof(void*));
-}
-#endif
-
-// ---- launch helpers (called from capi.cpp) -----------------------------------
-template <class Model>
-static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
-  // lane group: the smallest power of two holding nodes 0..N; G > 64 spans G/64 waves.
-  // A batch too small to give every SIMD a wave gets wider groups (up to one instance per
-  // wave): the per-wave instruction stream is the same, but a wave then runs only its own
-  // instance's iterations, not the maximum over the instances it holds (config 2: +5 %
-  // solves/s in multi-step launches).  spec.group_policy = 1 keeps the narrowest group.
-  int G = a.N < 16 ? 16 : a.N < 32 ? 32 : a.N < 64 ? 64 : a.N < 128 ? 128 : 256;
-  if (a.group_policy == 0)
-    while (G < 64 && (long)a.B * G * 2 <= 64L * a.n_simd) G *= 2;
-  const long threads = (long)a.B * G;
-  const int bs = G > 64 ? G : 64;
-  const int blocks = (int)((threads + bs - 1) / bs);
-  if (G == 16) hipLaunchKernelGGL((solve_kernel<Model, 16>), dim3(blocks), dim3(64), 0, stream, a);
-  else if (G == 32) hipLaunchKernelGGL((solve_kernel<Model, 32>), dim3(blocks), dim3(64), 0, stream, a);
-  else if (G == 64) hipLaunchKernelGGL((solve_kernel<Model, 64>), dim3(blocks), dim3(64), 0, stream, a);
-  else if (G == 128) hipLaunchKernelGGL((solve_kernel<Model, 128>), dim3(blocks), dim3(128), 0, stream, a);
-  else hipLaunchKernelGGL((solve_kernel<Model, 256>), dim3(blocks), dim3(256), 0, stream, a);
-  return hipGetLastError();
-}
-
-// model dispatch: unicycle, and the linear-model shapes the reference's QPs need
-// (4x1 lateral / cart-pole, 5x1 cart-pole with the previous input as a state).
-#ifdef MPCX_ONLY_UNICYCLE  // diagnostic builds (register-usage experiments): unicycle kernels only
-#define MPCX_DISPATCH(a, FN, ...)                                 \
-  do {                                                            \
-    if ((a).model == 1) return FN<UnicycleModel>(__VA_ARGS__);    \
-    return hipErrorInvalidValue;                                  \
-  } while (0)
-#else
-#define MPCX_DISPATCH(a, FN, ...)                                                                \
-  do {                                                                                           \
-    if ((a).model == 1) return FN<UnicycleModel>(__VA_ARGS__);                                   \
-    if ((a).model == 2 && (a).nx == 4 && (a).nu == 1) return FN<LinearModel<4, 1>>(__VA_ARGS__); \
-    if ((a).model == 2 && (a).nx == 5 && (a).nu == 1) return FN<LinearModel<5, 1>>(__VA_ARGS__); \
-    if ((a).model == 3) return FN<OdeModel<KinBicycle>>(__VA_ARGS__);                            \
-    if ((a).model == 4) return FN<OdeModel<DynBicycle>>(__VA_ARGS__);                            \
-    if ((a).model == 5) return FN<OdeModel<CartPole>>(__VA_ARGS__);                              \
-    return hipErrorInvalidValue;                                                                 \
-  } while (0)
-#endif
-
-hipError_t launch_solve(const SolveArgs& a, hipStream_t stream) { MPCX_DISPATCH(a, launch_solve_model, a, stream); }
-
-template <class Model>
-static hipError_t launch_plant_model(const SolveArgs& a, const double* U, double* XF, double* QF, hipStream_t stream) {
-  hipLaunchKernelGGL((plant_kernel<Model>), dim3((a.B + 255) / 256), dim3(256), 0, stream, a, U, XF, QF);
-  return hipGetLastError();
-}
-hipError_t launch_plant(const SolveArgs& a, const double* U, double* XF, double* QF, hipStream_t stream) {
-  MPCX_DISPATCH(a, launch_plant_model, a, U, XF, QF, stream);
-}
-
-template <class Model>
-static hipError_t launch_constraints_model(const SolveArgs& a, const double* W, double* Gout, hipStream_t stream) {
-  hipLaunchKernelGGL((constraints_kernel<Model>), dim3((a.B + 255) / 256), dim3(256), 0, stream, a, W, Gout);
-  return hipGetLastError();
-}
-hipError_t launch_constraints(const SolveArgs& a, const double* W, double* Gout, hipStream_t stream) {
-  MPCX_DISPATCH(a, launch_constraints_model, a, W, Gout, stream);
-}
-
-template <class Model>
-static hipError_t launch_shift_model(const SolveArgs& a, double* P, const double* W, double* W0, const double* L,
-                                     double* L0, const double* LX, double* LX0, hipStream_t stream) {
-  hipLaunchKernelGGL((shift_kernel<Model>), dim3((a.B + 255) / 256), dim3(256), 0, stream, a, P, W, W0, L, L0, LX,
-                     LX0);
-  return hipGetLastError();
-}
-hipError_t launch_shift(const SolveArgs& a, double* P, const double* W, double* W0, const double* L, double* L0,
-                        const double* LX, double* LX0, hipStream_t stream) {
-  MPCX_DISPATCH(a, launch_shift_model, a, P, W, W0, L, L0, LX, LX0, stream);
-}
-
 hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X, const double* U, const double* XR,
                            double* J, hipStream_t stream) {
   const long blocks = ((long)B + 255) / 256;
@@ -1660,4 +87,59 @@ hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X,
   return hipGetLastError();
 }
 
+// ---- model dispatch (the entry points live in solve_<model>.hip) -------------------
+#define MPCX_DECLARE(tag)                                                                                       \
+  hipError_t launch_solve_##tag(const SolveArgs&, hipStream_t);                                                 \
+  hipError_t launch_plant_##tag(const SolveArgs&, const double*, double*, double*, hipStream_t);                \
+  hipError_t launch_constraints_##tag(const SolveArgs&, const double*, double*, hipStream_t);                    \
+  hipError_t launch_shift_##tag(const SolveArgs&, double*, const double*, double*, const double*, double*,       \
+                                const double*, double*, hipStream_t);                                           \
+  int diag_set_stamps_##tag(void*);                                                                             \
+  int diag_set_counters_##tag(void*);
+MPCX_DECLARE(unicycle)
+MPCX_DECLARE(linear4)
+MPCX_DECLARE(linear5)
+MPCX_DECLARE(kin_bicycle)
+MPCX_DECLARE(dyn_bicycle)
+MPCX_DECLARE(cartpole)
+
+// unicycle, the linear-model shapes the reference's QPs need (4x1 lateral / cart-pole, 5x1
+// cart-pole with the previous input as a state), and the BASELINE's nonlinear ODE variants
+#define MPCX_DISPATCH(a, FN, ...)                                                 \
+  do {                                                                            \
+    if ((a).model == 1) return FN##_unicycle(__VA_ARGS__);                        \
+    if ((a).model == 2 && (a).nx == 4 && (a).nu == 1) return FN##_linear4(__VA_ARGS__); \
+    if ((a).model == 2 && (a).nx == 5 && (a).nu == 1) return FN##_linear5(__VA_ARGS__); \
+    if ((a).model == 3) return FN##_kin_bicycle(__VA_ARGS__);                     \
+    if ((a).model == 4) return FN##_dyn_bicycle(__VA_ARGS__);                     \
+    if ((a).model == 5) return FN##_cartpole(__VA_ARGS__);                        \
+    return hipErrorInvalidValue;                                                  \
+  } while (0)
+
+hipError_t launch_solve(const SolveArgs& a, hipStream_t stream) { MPCX_DISPATCH(a, launch_solve, a, stream); }
+hipError_t launch_plant(const SolveArgs& a, const double* U, double* XF, double* QF, hipStream_t stream) {
+  MPCX_DISPATCH(a, launch_plant, a, U, XF, QF, stream);
+}
+hipError_t launch_constraints(const SolveArgs& a, const double* W, double* Gout, hipStream_t stream) {
+  MPCX_DISPATCH(a, launch_constraints, a, W, Gout, stream);
+}
+hipError_t launch_shift(const SolveArgs& a, double* P, const double* W, double* W0, const double* L, double* L0,
+                        const double* LX, double* LX0, hipStream_t stream) {
+  MPCX_DISPATCH(a, launch_shift, a, P, W, W0, L, L0, LX, LX0, stream);
+}
+
 }  // namespace mpcx
+
+#ifdef MPCX_STAMPS
+// diagnostic build: every model unit holds its own copy of the buffer pointers
+extern "C" int mpcx_diag_set_stamp_buffer(void* d_buf) {
+  using namespace mpcx;
+  return diag_set_stamps_unicycle(d_buf) | diag_set_stamps_linear4(d_buf) | diag_set_stamps_linear5(d_buf) |
+         diag_set_stamps_kin_bicycle(d_buf) | diag_set_stamps_dyn_bicycle(d_buf) | diag_set_stamps_cartpole(d_buf);
+}
+extern "C" int mpcx_diag_set_counter_buffer(void* d_buf) {
+  using namespace mpcx;
+  return diag_set_counters_unicycle(d_buf) | diag_set_counters_linear4(d_buf) | diag_set_counters_linear5(d_buf) |
+         diag_set_counters_kin_bicycle(d_buf) | diag_set_counters_dyn_bicycle(d_buf) | diag_set_counters_cartpole(d_buf);
+}
+#endif

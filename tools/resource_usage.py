@@ -8,8 +8,9 @@ import sys
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-out = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "mpc-verde_amd"), "resource-usage"], capture_output=True,
-                     text=True).stderr
+out = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "mpc-verde_amd"), "-j8", "resource-usage"],
+                     capture_output=True, text=True)
+out = out.stdout + out.stderr
 rows, cur = [], None
 for line in out.splitlines():
     m = re.search(r"remark:\s+(Function Name|VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]): (\S+)",
