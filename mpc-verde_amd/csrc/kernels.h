@@ -1290,6 +1290,12 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     }
     }
     if (!done && !accepted) {
+#ifdef MPCX_STAMPS
+      if (k == 0)
+        printf("LSFAIL inst=%d step=%d it=%d mu=%.3e thk=%.6e phk=%.10e gd=%.3e amax=%.3e alpha=%.3e amin=%.3e "
+               "Ed=%.3e Ec=%.3e Ecomp=%.3e E0=%.3e fs=%.3e dw=%.1e\n",
+               inst, step, it, mu, thk, phk, gd, amax, alpha, amin, Ed, Ec, Ecomp0, E0, fs, delta);
+#endif
       done = true;
       status = 3;
       its = it;
