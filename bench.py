@@ -303,7 +303,11 @@ def main():
         ocp = mpcx.lateral_ltv(N=N, Delta=0.05, vref=vref, per_instance_tab=np.minimum(t0, 499))
     else:
         ocp = mpcx.inverted_pendulum_qp(N=N)
-    solver = mpcx.nlpsol("bench", "mi355x", ocp, {"ipopt": {"max_iter": 3000}}, device=local)
+    # config 2 is Casadi/multiple_shooting_casadi.py: its own IPOPT options (:188-196); the
+    # others run IPOPT's defaults (mpctools / no reference script)
+    ipopt = ({"max_iter": 2000, "acceptable_tol": 1e-8, "acceptable_obj_change_tol": 1e-6}
+             if cfg == 2 and variant is None else {"max_iter": 3000})
+    solver = mpcx.nlpsol("bench", "mi355x", ocp, {"ipopt": ipopt}, device=local)
     stream = torch.cuda.current_stream()
 
     if args.profile_sweep_only:

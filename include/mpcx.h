@@ -75,10 +75,14 @@ enum mpcx_param_layout {
 };
 
 enum mpcx_status {
-  MPCX_CONVERGED = 0,   /* optimality error <= tol (IPOPT "Solve_Succeeded") */
-  MPCX_ACCEPTABLE = 1,  /* reserved */
+  MPCX_CONVERGED = 0,   /* optimality error <= tol and the unscaled tests hold (IPOPT "Solve_Succeeded") */
+  MPCX_ACCEPTABLE = 1,  /* acceptable level for acceptable_iter iterations, or an acceptable point at a
+                           failed line search ("Solved_To_Acceptable_Level") */
   MPCX_MAX_ITER = 2,    /* iteration limit reached */
-  MPCX_FAILED = 3       /* line search / inertia correction failed, or non-finite values */
+  MPCX_FAILED = 3,      /* line search failed and could not be recovered ("Restoration_Failed") */
+  MPCX_INFEASIBLE = 4,  /* the restoration phase converged to a point of local infeasibility
+                           ("Infeasible_Problem_Detected") */
+  MPCX_STEP_FAILED = 5  /* inertia correction failed ("Error_In_Step_Computation") */
 };
 
 enum mpcx_err {
@@ -110,6 +114,21 @@ typedef struct mpcx_spec {
   double warm_mu_init, warm_bound_push, warm_mult_push;
   int32_t nx, nu;       /* state / control dimensions (unicycle: 3, 2) */
   double par[8];        /* model constants of the ODE models (see mpcx_model) */
+  /* IPOPT termination and recovery options (IPOPT's names and semantics; the reference passes
+     max_iter, acceptable_tol = 1e-8 and acceptable_obj_change_tol = 1e-6 at
+     Casadi/multiple_shooting_casadi.py:188-196).  A field left 0 takes IPOPT's default:
+     dual_inf_tol 1, constr_viol_tol 1e-4, compl_inf_tol 1e-4 (unscaled tests next to tol),
+     acceptable_tol 1e-6, acceptable_dual_inf_tol 1e10, acceptable_constr_viol_tol 1e-2,
+     acceptable_compl_inf_tol 1e-2, acceptable_obj_change_tol 1e20, acceptable_iter 15
+     (-1 disables the acceptable-level termination). */
+  double dual_inf_tol, constr_viol_tol, compl_inf_tol;
+  double acceptable_tol, acceptable_dual_inf_tol, acceptable_constr_viol_tol, acceptable_compl_inf_tol;
+  double acceptable_obj_change_tol;
+  int32_t acceptable_iter;
+  /* 0: a failed line search enters IPOPT's soft restoration and then the feasibility
+     restoration phase (models that have one: the ODE models); 1: the solve ends there
+     (MPCX_FAILED unless the point is acceptable) */
+  int32_t no_restoration;
 } mpcx_spec;
 
 /* Fill *s with the reference's constants for model/cost at horizon N

@@ -40,6 +40,9 @@ struct mpcx_handle {
   const int32_t* ext_tab = nullptr;  // caller-owned device schedule (mpcx_set_linear_tab_dev)
   int ext_rows = 0;
   int n_simd = 0;  // SIMDs of the device (CUs x 4): the solve launch widens lane groups to fill them
+  // restoration workspace of the models with a restoration phase (grown on demand)
+  size_t cap_ws = 0;
+  double* d_ws = nullptr;
 };
 
 namespace {
@@ -255,6 +258,21 @@ int mpcx_default_spec(mpcx_spec* s, int32_t model, int32_t N) {
   s->warm_mu_init = 1e-4;
   s->warm_bound_push = 1e-4;
   s->warm_mult_push = 1e-4;
+  // IPOPT termination options: the reference's acceptable_tol / acceptable_obj_change_tol
+  // (:192-193), IPOPT's defaults for the rest
+  s->dual_inf_tol = 1.0;
+  s->constr_viol_tol = 1e-4;
+  s->compl_inf_tol = 1e-4;
+  s->acceptable_tol = 1e-8;
+  s->acceptable_dual_inf_tol = 1e10;
+  s->acceptable_constr_viol_tol = 1e-2;
+  s->acceptable_compl_inf_tol = 1e-2;
+  s->acceptable_obj_change_tol = 1e-6;
+  s->acceptable_iter = 15;
+  if (is_ode(model)) {  // no reference script: IPOPT's defaults
+    s->acceptable_tol = 1e-6;
+    s->acceptable_obj_change_tol = 1e20;
+  }
   if (is_ode(model)) {  // defaults of the BASELINE config variants (mpcx/ode.py documents them)
     s->cost = MPCX_COST_NODE;
     s->param_layout = MPCX_P_X0_STAGEREF;
@@ -311,6 +329,15 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
   if (s->max_iter < 0) return fail(MPCX_EINVAL, "max_iter < 0");
   if (s->group_policy != 0 && s->group_policy != 1) return fail(MPCX_EINVAL, "group_policy must be 0 or 1");
   if (!(s->tol > 0)) return fail(MPCX_EINVAL, "tol must be > 0");
+  {
+    const double o[8] = {s->dual_inf_tol, s->constr_viol_tol, s->compl_inf_tol, s->acceptable_tol,
+                         s->acceptable_dual_inf_tol, s->acceptable_constr_viol_tol, s->acceptable_compl_inf_tol,
+                         s->acceptable_obj_change_tol};
+    for (double v : o)
+      if (!(v >= 0)) return fail(MPCX_EINVAL, "IPOPT tolerance options must be >= 0 (0 = IPOPT default)");
+    if (s->acceptable_iter < -1) return fail(MPCX_EINVAL, "acceptable_iter must be >= -1");
+    if (s->no_restoration != 0 && s->no_restoration != 1) return fail(MPCX_EINVAL, "no_restoration must be 0 or 1");
+  }
   if (!(s->warm_mu_init > 0) || !(s->warm_bound_push > 0) || !(s->warm_mult_push > 0))
     return fail(MPCX_EINVAL, "warm_mu_init / warm_bound_push / warm_mult_push must be > 0");
   for (int i = 0; i < nu_of(*s); ++i)
@@ -360,6 +387,7 @@ void mpcx_destroy(mpcx_handle* h) {
   dev_free(h->d_ubw_call);
   free_workspace(h);
   dev_free(h->d_sweep);
+  dev_free(h->d_ws);
   free_linear(h);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -464,6 +492,20 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
   a.p_layout = h->spec.param_layout;
   a.p_stride = h->np;
   a.tol = h->spec.tol;
+  {  // IPOPT options, 0 = IPOPT default
+    const mpcx_spec& sp = h->spec;
+    auto d = [](double v, double def) { return v > 0 ? v : def; };
+    a.dual_inf_tol = d(sp.dual_inf_tol, 1.0);
+    a.constr_viol_tol = d(sp.constr_viol_tol, 1e-4);
+    a.compl_inf_tol = d(sp.compl_inf_tol, 1e-4);
+    a.acc_tol = d(sp.acceptable_tol, 1e-6);
+    a.acc_dual_inf_tol = d(sp.acceptable_dual_inf_tol, 1e10);
+    a.acc_constr_viol_tol = d(sp.acceptable_constr_viol_tol, 1e-2);
+    a.acc_compl_inf_tol = d(sp.acceptable_compl_inf_tol, 1e-2);
+    a.acc_obj_change_tol = d(sp.acceptable_obj_change_tol, 1e20);
+    a.acc_iter = sp.acceptable_iter == 0 ? 15 : (sp.acceptable_iter < 0 ? 0 : sp.acceptable_iter);
+    a.restoration = sp.no_restoration ? 0 : 1;
+  }
   a.sp = stage_params(h->spec);
   a.op = ode_params(h->spec);
   a.P = P;
@@ -485,6 +527,31 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
   return a;
 }
 
+// launch the solve with the restoration workspace of the model (grown on demand; freed only
+// after the device is idle, since a queued launch may still use it)
+static int solve_launch(mpcx_handle* h, mpcx::SolveArgs& a, hipStream_t stream) {
+  const int slots = mpcx::resto_ws_slots(a.model, a.nx, a.nu);
+  if (slots > 0 && a.restoration) {
+    const int G = mpcx::solve_group_size(a.N, a.B, a.n_simd, a.group_policy);
+    const long bs = G > 64 ? G : 64;
+    const long threads = ((long)a.B * G + bs - 1) / bs * bs;
+    const size_t need = (size_t)slots * threads;
+    if (need > h->cap_ws) {
+      HIPCHK(hipDeviceSynchronize());
+      dev_free(h->d_ws);
+      h->cap_ws = 0;
+      HIPCHK(hipMalloc(&h->d_ws, need * sizeof(double)));
+      h->cap_ws = need;
+    }
+    a.ws = h->d_ws;
+    a.ws_stride = threads;
+  } else {
+    a.restoration = 0;
+  }
+  HIPCHK(mpcx::launch_solve(a, stream));
+  return 0;
+}
+
 int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const double* d_w0, const double* d_lam_g0,
                          const double* d_lam_x0, double* d_w_out, double* d_f_out, double* d_lam_g,
                          double* d_lam_x, int32_t* d_status, int32_t* d_iters, void* stream) {
@@ -495,7 +562,7 @@ int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const dou
   DEVICE_SCOPE(h->spec.device);
   mpcx::SolveArgs a = make_args(h, B, d_P, d_w0, d_lam_g0, d_lam_x0, h->d_lbw, h->d_ubw, d_w_out, d_f_out, d_lam_g,
                                 d_lam_x, d_status, d_iters);
-  HIPCHK(mpcx::launch_solve(a, (hipStream_t)stream));
+  if (int r = solve_launch(h, a, (hipStream_t)stream)) return r;
   return 0;
 }
 
@@ -517,7 +584,7 @@ int mpcx_step_dev(mpcx_handle* h, int32_t B, double* d_P, double* d_w0, double* 
   a.w0_next = d_w0;
   a.lam0_next = d_lam_g0;
   a.lamx0_next = d_lam_x0;
-  HIPCHK(mpcx::launch_solve(a, (hipStream_t)stream));
+  if (int r = solve_launch(h, a, (hipStream_t)stream)) return r;
   return 0;
 }
 
@@ -545,7 +612,7 @@ int mpcx_run_dev(mpcx_handle* h, int32_t B, int32_t K, double* d_P, double* d_w0
   a.warm_next = duals ? 1 : 0;
   a.Pseq = d_Pseq;
   a.tabseq = d_tabseq;
-  HIPCHK(mpcx::launch_solve(a, (hipStream_t)stream));
+  if (int r = solve_launch(h, a, (hipStream_t)stream)) return r;
   return 0;
 }
 
@@ -588,7 +655,7 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
   mpcx::SolveArgs a = make_args(h, B, h->d_P, w0 ? h->d_w0 : nullptr, lam_g0 ? h->d_lam0 : nullptr,
                                 lam_x0 ? h->d_lamx0 : nullptr, dl, du, h->d_w, h->d_f, (lam_g ? h->d_lam : nullptr),
                                 (lam_x ? h->d_lamx : nullptr), h->d_status, h->d_iters);
-  HIPCHK(mpcx::launch_solve(a, s));
+  if (int r = solve_launch(h, a, s)) return r;
   if (lam_x) HIPCHK(hipMemcpyAsync(lam_x, h->d_lamx, (size_t)B * h->nw * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(w_out, h->d_w, (size_t)B * h->nw * sizeof(double), hipMemcpyDeviceToHost, s));
   if (f_out) HIPCHK(hipMemcpyAsync(f_out, h->d_f, (size_t)B * sizeof(double), hipMemcpyDeviceToHost, s));

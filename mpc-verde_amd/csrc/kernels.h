@@ -310,6 +310,11 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   // IPOPT's filter-reset heuristic: iterations in a row whose last rejected trial point was
   // rejected by the filter alone, and resets so far in this solve
   int frej = 0, nfreset = 0;
+  // IPOPT termination: acceptable iterates in a row, scaled objective of the previous iterate
+  // (acceptable_obj_change_tol); a tiny step forces the next barrier decrease
+  int acc_count = 0;
+  double f_last = -1e50;
+  bool tiny_flag = false;
   int status = valid ? 2 : 0;
   bool done = !valid;
   int it = 0;        // iteration of this instance's current solve
@@ -394,6 +399,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       dw_last = 0.0;
       nfilt = fnext = 0;
       frej = nfreset = 0;
+      acc_count = 0;
+      f_last = -1e50;
+      tiny_flag = false;
       status = 2;
       done = false;
       it = 0;
@@ -510,10 +518,27 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     const double sd = fmax(kSmax, (lam1 + z1) / (double)(ng + nw)) / kSmax;
     const double sc = fmax(kSmax, nbound > 0 ? z1 / nbound : 0.0) / kSmax;
     const double E0 = fmax(fmax(Ed / sd, Ec), Ecomp0 / sc);
-    if (!done && E0 <= a.tol) {
+    // IPOPT OptimalityErrorConvergenceCheck: tol with the unscaled dual infeasibility,
+    // constraint violation and complementarity tests; then the acceptable level (all of
+    // acceptable_* and the objective change from the previous iterate) for acceptable_iter
+    // iterates in a row.  fcur = the scaled objective.
+    const double fcur = fs * gsum<G>(hasU ? qv : 0.0, xw);
+    const bool acceptable_now = E0 <= a.acc_tol && Ed <= a.acc_dual_inf_tol * fs && Ec <= a.acc_constr_viol_tol &&
+                                Ecomp0 <= a.acc_compl_inf_tol * fs &&
+                                fabs(fcur - f_last) <= a.acc_obj_change_tol * fmax(1.0, fabs(fcur));
+    if (!done && E0 <= a.tol && Ed <= a.dual_inf_tol * fs && Ec <= a.constr_viol_tol && Ecomp0 <= a.compl_inf_tol * fs) {
       done = true;
       status = 0;
       its = it;
+    }
+    if (!done) {
+      f_last = fcur;
+      acc_count = (a.acc_iter > 0 && acceptable_now) ? acc_count + 1 : 0;
+      if (a.acc_iter > 0 && acc_count >= a.acc_iter) {
+        done = true;
+        status = 1;
+        its = it;
+      }
     }
     if (!done && it >= a.max_iter) {
       done = true;
@@ -531,6 +556,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 
     STAMP(1);
     // ------------------------------------------------------------ barrier update
+    // (IPOPT monotone update with mu_allow_fast_monotone_decrease: repeated while the barrier
+    //  test holds; a tiny step forces the first decrease)
     for (int rep = 0; rep < 32; ++rep) {
       double Ecm = 0;
 #pragma unroll
@@ -540,7 +567,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       }
       Ecm = gmax<G>(Ecm, xw);
       const double Emu = fmax(fmax(Ed / sd, Ec), Ecm / sc);
-      const bool dec = !done && Emu <= kKappaEps * mu && mu > mu_min;
+      const bool dec = !done && (Emu <= kKappaEps * mu || (tiny_flag && rep == 0)) && mu > mu_min;
       if (dec && !done) DIAG(3);
       if (dec) {
         static_assert(kThetaMu == 1.5, "mu^theta_mu evaluated as mu * sqrt(mu)");
@@ -549,8 +576,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         nfilt = 0;
         fnext = 0;
       }
-      if (!__any(dec && it == 0)) break;
+      if (!__any(dec)) break;
     }
+    tiny_flag = false;
 
     STAMP(2);
     // ------------------------------------------------------------ barrier gradient, Sigma
@@ -775,7 +803,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     }
     if (!done && failed) {
       done = true;
-      status = 3;
+      status = 5;  // inertia correction failed (IPOPT Error_In_Step_Computation)
       its = it;
     }
     if constexpr (kDec) pcv = !failed && delta == 0.0;  // Pk now holds a delta = 0 factorisation
@@ -964,6 +992,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     bool searching = !done && !tinystep;
     bool accepted = !done && tinystep;
     bool ftype = tinystep;
+    tiny_flag = !done && tinystep;
     bool trial_fresh = false;  // accepted at the first trial, which evaluated derivatives
     bool lastrej_f = false;    // the last rejected trial passed the sufficient decrease test but not the filter
     // switching condition alpha (-gd)^s_phi > delta theta^s_theta  <=>  alpha > sw_a with
@@ -1297,7 +1326,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
                inst, step, it, mu, thk, phk, gd, amax, alpha, amin, Ed, Ec, Ecomp0, E0, fs, delta);
 #endif
       done = true;
-      status = 3;
+      // IPOPT: "restoration phase called at an acceptable point" ends the solve at that point
+      status = acceptable_now ? 1 : 3;
       its = it;
     }
 
@@ -1520,9 +1550,7 @@ static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
   // wave): the per-wave instruction stream is the same, but a wave then runs only its own
   // instance's iterations, not the maximum over the instances it holds (config 2: +5 %
   // solves/s in multi-step launches).  spec.group_policy = 1 keeps the narrowest group.
-  int G = a.N < 16 ? 16 : a.N < 32 ? 32 : a.N < 64 ? 64 : a.N < 128 ? 128 : 256;
-  if (a.group_policy == 0)
-    while (G < 64 && (long)a.B * G * 2 <= 64L * a.n_simd) G *= 2;
+  const int G = solve_group_size(a.N, a.B, a.n_simd, a.group_policy);
   const long threads = (long)a.B * G;
   const int bs = G > 64 ? G : 64;
   const int blocks = (int)((threads + bs - 1) / bs);

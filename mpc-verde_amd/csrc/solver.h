@@ -35,6 +35,13 @@ struct SolveArgs {
   int n_simd;           // SIMDs of the device (0 = unknown): lane groups widen to fill them
   int group_policy;     // mpcx_spec.group_policy
   double tol;
+  // IPOPT termination options (mpcx_spec, defaults resolved by the host)
+  double dual_inf_tol, constr_viol_tol, compl_inf_tol;
+  double acc_tol, acc_dual_inf_tol, acc_constr_viol_tol, acc_compl_inf_tol, acc_obj_change_tol;
+  int acc_iter;         // <= 0: no acceptable-level termination
+  int restoration;      // soft restoration + restoration phase on a failed line search (models with kResto)
+  double* ws;           // restoration workspace: slot i of thread t at ws[i * ws_stride + t] (kResto models)
+  long ws_stride;
   StageParams sp;       // unicycle constants
   LinTables lin;        // linear model tables
   OdeParams op;         // nonlinear ODE models
@@ -77,6 +84,36 @@ struct ModelArgs {
   int tc_stride = 0;     // slot stride (threads per block)
 };
 __host__ __device__ inline ModelArgs model_args(const SolveArgs& a) { return ModelArgs{a.sp, a.lin, a.op, a.p_layout, a.N}; }
+
+// lane group of the solve launch: the smallest power of two holding nodes 0..N; a batch too
+// small to give every SIMD a wave gets wider groups (up to one instance per wave) unless
+// group_policy = 1.  G > 64 spans G/64 waves (one workgroup per instance).
+inline int solve_group_size(int N, long B, int n_simd, int group_policy) {
+  int G = N < 16 ? 16 : N < 32 ? 32 : N < 64 ? 64 : N < 128 ? 128 : 256;
+  if (group_policy == 0)
+    while (G < 64 && B * G * 2 <= 64L * n_simd) G *= 2;
+  return G;
+}
+// Restoration-phase workspace (models with kResto), structure of arrays over threads: slot i
+// of thread t at ws[i * ws_stride + t].  Per lane k: p, n, z_p, z_n of the rows of g_{k+1}
+// (the interval k defect), lane 0 also those of g_0; the proximity reference z_R and the bound
+// multipliers at the restoration start; the original filter entry kept in this lane; the
+// iterate saved before a soft-restoration step (restored if the step is rejected).
+struct RestoWs {
+  static constexpr int P = 0;
+  __host__ __device__ static constexpr int N_(int nx) { return nx; }
+  __host__ __device__ static constexpr int ZP(int nx) { return 2 * nx; }
+  __host__ __device__ static constexpr int ZN(int nx) { return 3 * nx; }
+  __host__ __device__ static constexpr int ROW0(int nx) { return 4 * nx; }  // g_0's p, n, z_p, z_n (lane 0)
+  __host__ __device__ static constexpr int ZR(int nx) { return 8 * nx; }
+  __host__ __device__ static constexpr int ZLR(int nx, int nz) { return 8 * nx + nz; }
+  __host__ __device__ static constexpr int ZUR(int nx, int nz) { return 8 * nx + 2 * nz; }
+  __host__ __device__ static constexpr int FIL(int nx, int nz) { return 8 * nx + 3 * nz; }
+  __host__ __device__ static constexpr int SAVE(int nx, int nz) { return 8 * nx + 3 * nz + 2; }  // z, lam, zL, zU
+  __host__ __device__ static constexpr int slots(int nx, int nu) { return SAVE(nx, nx + nu) + 3 * (nx + nu) + nx; }
+};
+// doubles of restoration workspace per thread (0: the model has no restoration phase)
+int resto_ws_slots(int model, int nx, int nu);
 
 hipError_t launch_solve(const SolveArgs& a, hipStream_t stream);
 hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X, const double* U, const double* XR,

@@ -87,6 +87,12 @@ hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X,
   return hipGetLastError();
 }
 
+// restoration workspace per thread: the ODE models (kernels.h RestoWs); none elsewhere
+int resto_ws_slots(int model, int nx, int nu) {
+  if (model < 3 || model > 5) return 0;
+  return RestoWs::slots(nx, nu);
+}
+
 // ---- model dispatch (the entry points live in solve_<model>.hip) -------------------
 #define MPCX_DECLARE(tag)                                                                                       \
   hipError_t launch_solve_##tag(const SolveArgs&, hipStream_t);                                                 \

@@ -24,7 +24,7 @@ P_X0_XREF = 0
 P_X0_STAGEREF = 1
 
 STATUS = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Maximum_Iterations_Exceeded",
-          3: "Solve_Failed"}
+          3: "Restoration_Failed", 4: "Infeasible_Problem_Detected", 5: "Error_In_Step_Computation"}
 
 # C-ABI entry points (include/mpcx.h) -- checked by tests/test_capi_symbols.py
 EXPORTS = ("mpcx_default_spec", "mpcx_create", "mpcx_destroy", "mpcx_last_error", "mpcx_dims", "mpcx_solve_batch",
@@ -45,7 +45,12 @@ class Spec(ctypes.Structure):
                 ("lbu", ctypes.c_double * 8), ("ubu", ctypes.c_double * 8), ("lbx", ctypes.c_double * 8),
                 ("ubx", ctypes.c_double * 8), ("warm_mu_init", ctypes.c_double),
                 ("warm_bound_push", ctypes.c_double), ("warm_mult_push", ctypes.c_double),
-                ("nx", ctypes.c_int32), ("nu", ctypes.c_int32), ("par", ctypes.c_double * 8)]
+                ("nx", ctypes.c_int32), ("nu", ctypes.c_int32), ("par", ctypes.c_double * 8),
+                ("dual_inf_tol", ctypes.c_double), ("constr_viol_tol", ctypes.c_double),
+                ("compl_inf_tol", ctypes.c_double), ("acceptable_tol", ctypes.c_double),
+                ("acceptable_dual_inf_tol", ctypes.c_double), ("acceptable_constr_viol_tol", ctypes.c_double),
+                ("acceptable_compl_inf_tol", ctypes.c_double), ("acceptable_obj_change_tol", ctypes.c_double),
+                ("acceptable_iter", ctypes.c_int32), ("no_restoration", ctypes.c_int32)]
 
 
 _lib = None

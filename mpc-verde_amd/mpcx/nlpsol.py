@@ -28,7 +28,7 @@ import numpy as np
 
 from . import _lib
 from .lti import LinearOCP
-from .ocp import OCP, to_spec
+from .ocp import IPOPT_OPTIONS, OCP, to_spec
 from .ode import OdeOCP
 
 
@@ -56,14 +56,20 @@ class Solver:
         self.ocp = ocp
         self.max_iter = int(ip.pop("max_iter", 3000))
         self.tol = float(ip.pop("tol", 1e-8))
-        # accepted for source compatibility with :188-196; they do not change the optimum
-        for k in ("print_level", "acceptable_tol", "acceptable_obj_change_tol", "acceptable_iter", "sb"):
+        # output options have no effect here (no iteration log is printed)
+        for k in ("print_level", "sb"):
             ip.pop(k, None)
+        # termination options (acceptable_tol / acceptable_obj_change_tol at :192-193), IPOPT's
+        # semantics; the rest keep IPOPT's defaults
+        term = {k: ip.pop(k) for k in IPOPT_OPTIONS if k in ip}
         if ip:
             raise ValueError(f"unsupported ipopt options: {sorted(ip)}")
-        # not a CasADi option: lanes per instance (0 = fill idle SIMDs, 1 = narrowest group; same results)
+        # not CasADi options: lanes per instance (0 = fill idle SIMDs, 1 = narrowest group; same
+        # results); restoration (False: a failed line search ends the solve, IPOPT has no such switch)
         self.group_policy = int(opts.get("group_policy", 0))
-        self._h = _lib.Handle(to_spec(ocp, self.max_iter, self.tol, device, group_policy=self.group_policy))
+        self.restoration = bool(opts.get("restoration", True))
+        self._h = _lib.Handle(to_spec(ocp, self.max_iter, self.tol, device, group_policy=self.group_policy, ipopt=term,
+                                      restoration=self.restoration))
         if ocp.model == "linear":
             self._h.set_linear_model(ocp)
         self._stats = {}

@@ -103,10 +103,23 @@ MODEL_IDS = {"unicycle": _lib.MODEL_UNICYCLE, "linear": _lib.MODEL_LINEAR, "kin_
              "dyn_bicycle": _lib.MODEL_DYN_BICYCLE, "cartpole": _lib.MODEL_CARTPOLE}
 
 
-def to_spec(ocp, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4), group_policy=0) -> _lib.Spec:
+# IPOPT termination / recovery options the spec carries (IPOPT's names); values left out take
+# IPOPT's defaults, except the reference's own acceptable_tol / acceptable_obj_change_tol
+# (Casadi/multiple_shooting_casadi.py:192-193) for the unicycle scripts' problems
+IPOPT_OPTIONS = ("dual_inf_tol", "constr_viol_tol", "compl_inf_tol", "acceptable_tol", "acceptable_dual_inf_tol",
+                 "acceptable_constr_viol_tol", "acceptable_compl_inf_tol", "acceptable_obj_change_tol",
+                 "acceptable_iter")
+IPOPT_DEFAULTS = {"dual_inf_tol": 1.0, "constr_viol_tol": 1e-4, "compl_inf_tol": 1e-4, "acceptable_tol": 1e-6,
+                  "acceptable_dual_inf_tol": 1e10, "acceptable_constr_viol_tol": 1e-2,
+                  "acceptable_compl_inf_tol": 1e-2, "acceptable_obj_change_tol": 1e20, "acceptable_iter": 15}
+
+
+def to_spec(ocp, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4), group_policy=0, ipopt=None,
+            restoration=True) -> _lib.Spec:
     """mpcx_spec of an :class:`OCP` (unicycle), :class:`mpcx.lti.LinearOCP` (linear model;
     its stage tables are uploaded separately by the solver, mpcx_set_linear_model) or
-    :class:`mpcx.ode.OdeOCP` (nonlinear ODE models, constants in ``par``)."""
+    :class:`mpcx.ode.OdeOCP` (nonlinear ODE models, constants in ``par``).  ``ipopt``: IPOPT
+    termination options by name (IPOPT_OPTIONS; IPOPT's defaults otherwise)."""
     if ocp.model not in MODEL_IDS:
         raise ValueError(f"unsupported model {ocp.model!r}")
     s = _lib.Spec()
@@ -121,6 +134,17 @@ def to_spec(ocp, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4), gro
     s.warm_mu_init, s.warm_bound_push, s.warm_mult_push = (float(v) for v in warm)
     s.nx, s.nu = int(ocp.nx), int(ocp.nu)
     s.group_policy = int(group_policy)
+    o = dict(IPOPT_DEFAULTS)
+    for k, v in (ipopt or {}).items():
+        if k not in o:
+            raise ValueError(f"unknown IPOPT option {k!r}")
+        o[k] = v
+    for k in IPOPT_OPTIONS:
+        if k == "acceptable_iter":
+            s.acceptable_iter = -1 if int(o[k]) == 0 else int(o[k])  # IPOPT: 0 disables the heuristic
+        else:
+            setattr(s, k, float(o[k]))
+    s.no_restoration = 0 if restoration else 1
     big = 1e20
 
     def fin(v, default):

@@ -65,8 +65,8 @@ def test_python_binding_matches_header():
 
     assert set(mpcx._lib.EXPORTS) == set(declared_symbols())
     # struct layout: 8 int32 + 2 double + 6 x double[8] + 3 double (warm start) + 2 int32 (nx, nu)
-    # + double[8] (par)
-    assert ctypes.sizeof(mpcx._lib.Spec) == 8 * 4 + 2 * 8 + 6 * 8 * 8 + 3 * 8 + 2 * 4 + 8 * 8
+    # + double[8] (par) + 8 double (IPOPT tolerances) + 2 int32 (acceptable_iter, no_restoration)
+    assert ctypes.sizeof(mpcx._lib.Spec) == 8 * 4 + 2 * 8 + 6 * 8 * 8 + 3 * 8 + 2 * 4 + 8 * 8 + 8 * 8 + 2 * 4
 
 
 def test_default_spec_without_gpu(lib):
@@ -76,6 +76,9 @@ def test_default_spec_without_gpu(lib):
     assert lib.mpcx_default_spec(ctypes.byref(s), 1, 20) == 0
     assert s.N == 20 and s.M == 4 and abs(s.T - 0.2) < 1e-15 and s.max_iter == 2000
     assert list(s.Q[:3]) == [1.0, 5.0, 0.1] and list(s.R[:2]) == [0.5, 0.05]
+    # the reference's IPOPT options (Casadi/multiple_shooting_casadi.py:190-193), IPOPT's defaults otherwise
+    assert (s.acceptable_tol, s.acceptable_obj_change_tol, s.acceptable_iter) == (1e-8, 1e-6, 15)
+    assert (s.dual_inf_tol, s.constr_viol_tol, s.compl_inf_tol, s.no_restoration) == (1.0, 1e-4, 1e-4, 0)
     assert lib.mpcx_default_spec(ctypes.byref(s), 99, 20) < 0
     # ODE models: dimensions, node cost and constants (include/mpcx.h mpcx_model)
     for model, nx, nu, par in ((3, 3, 2, [0.5]), (4, 6, 2, [1200.0, 1.5, 2.0, 55000.0, 1350.0]),
