@@ -541,6 +541,7 @@ static int solve_launch(mpcx_handle* h, mpcx::SolveArgs& a, hipStream_t stream) 
       dev_free(h->d_ws);
       h->cap_ws = 0;
       HIPCHK(hipMalloc(&h->d_ws, need * sizeof(double)));
+      HIPCHK(hipMemset(h->d_ws, 0, need * sizeof(double)));  // no instance parked
       h->cap_ws = need;
     }
     a.ws = h->d_ws;
@@ -549,6 +550,8 @@ static int solve_launch(mpcx_handle* h, mpcx::SolveArgs& a, hipStream_t stream) 
     a.restoration = 0;
   }
   HIPCHK(mpcx::launch_solve(a, stream));
+  // instances parked at a failed line search continue in the resume launch (restoration)
+  if (a.restoration) HIPCHK(mpcx::launch_resume(a, stream));
   return 0;
 }
 

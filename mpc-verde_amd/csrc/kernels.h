@@ -39,7 +39,7 @@
 static __device__ unsigned long long* g_mpcx_stamps = nullptr;
 // per-instance event counters (diagnostic build; indices at the kernel's `diag` array)
 static __device__ int* g_mpcx_diag = nullptr;
-constexpr int kDiag = 12;  // counters per instance
+constexpr int kDiag = 14;  // counters per instance
 #define DIAG(i) (++diag[(i)])
 #define DIAG_IF(c, i) \
   do {                \
@@ -119,12 +119,19 @@ __device__ __forceinline__ double barrier_logsum(const double* z, const double* 
   return log(m) + (double)e * 0.69314718055994530942;
 }
 
+}  // namespace mpcx
+#include "resto.h"  // IPOPT's soft restoration and restoration phase (cold, out of line)
+namespace mpcx {
+
+// rarely taken branches: laid out away from the hot loop
+#define MPCX_COLD(c) __builtin_expect(!!(c), 0)
+
 #ifndef MPCX_WAVES_PER_EU
 #define MPCX_WAVES_ATTR
 #else
 #define MPCX_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(MPCX_WAVES_PER_EU, MPCX_WAVES_PER_EU)))
 #endif
-template <class Model, int G>
+template <class Model, int G, bool RESUME = false>
 __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(SolveArgs a) {
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2, NP = NX * (NX + 1) / 2;
   static_assert(NP + NX <= kXchStride && 2 * NZ + NX <= kXchStride && NX * NX + NX <= kXchStride,
@@ -315,6 +322,17 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   int acc_count = 0;
   double f_last = -1e50;
   bool tiny_flag = false;
+  // IPOPT's soft restoration and restoration phase (models with one: resto.h, out of line; the
+  // iterate travels through the workspace a.ws).  In the soft phase the soft step replaces the
+  // line search.
+  constexpr bool kRes = RestoOf<Model>::value;
+  const bool res_on = kRes && a.restoration != 0;  // kernel-uniform
+  bool soft = false;
+  int soft_count = 0;
+  bool parked = false;       // left to the resume launch at a failed line search (solve launch)
+  bool pending_rec = false;  // resume launch: recover at the top of the next pass
+  bool active = true;        // resume launch: this group is one the solve launch parked
+  bool scaled = false;       // the solve's objective scaling is set (its first pass ran)
   int status = valid ? 2 : 0;
   bool done = !valid;
   int it = 0;        // iteration of this instance's current solve
@@ -331,7 +349,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   // 4 fraction-to-boundary-limited steps (alpha_max < 1), 5 tiny steps, 6 filter rejections,
   // 7 f-type (Armijo) acceptances, 8 factorisations by the sequential fallback of the scan,
   // 9 filter resets, 10 first trials rejected with increased infeasibility (SOC-eligible),
-  // 11 accepted second-order corrections
+  // 11 accepted second-order corrections, 12 recoveries (soft restoration / restoration phase
+  // calls, resto.h), 13 restoration-phase iterations
   int diag[kDiag] = {};
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = 0;
@@ -344,7 +363,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   //      the fused epilogue below writes), load the next step's references and schedule,
   //      and restart the solve exactly as a new launch would from those buffers.
   auto step_boundary = [&]() __attribute__((always_inline)) {
-    const bool bnd = done && step < K - 1;  // group-uniform
+    const bool bnd = done && !parked && step < K - 1;  // group-uniform
     if (!__any(bnd)) return;
     constexpr int NS = NZ + NX + NZ;
     double own[NS], nxt[NS];
@@ -402,6 +421,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       acc_count = 0;
       f_last = -1e50;
       tiny_flag = false;
+      soft = false;
+      soft_count = 0;
+      scaled = false;
       status = 2;
       done = false;
       it = 0;
@@ -412,9 +434,146 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   // every pass is one IPM iteration for the instances still solving; instances that
   // finished a step of a multi-step launch restart at the top of the next pass.  Bounded:
   // each step ends after at most max_iter + 1 passes.
+  // ---- resume launch: only the groups the solve launch parked run, from their saved state
+  if constexpr (RESUME) {
+    double* const wsl = a.ws + gid;
+    const long wst = a.ws_stride;
+    auto W = [&](int i) __attribute__((always_inline)) -> double& { return wsl[(long)i * wst]; };
+    constexpr int S = RestoWs::SC(NX, NZ);
+    active = valid && W(S + RestoWs::sPEND) != 0.0;
+    if (!__any(active)) return;  // wave-uniform (a multi-wave group's waves agree)
+    if (active) {
+      W(S + RestoWs::sPEND) = 0.0;
+#ifdef MPCX_STAMPS
+      if (g_mpcx_diag)
+        for (int i = 0; i < kDiag; ++i) diag[i] = g_mpcx_diag[(size_t)inst * kDiag + i];
+#endif
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) {
+        z[i] = W(RestoWs::XZ + i);
+        zL[i] = W(RestoWs::XZL(NX, NZ) + i);
+        zU[i] = W(RestoWs::XZU(NX, NZ) + i);
+      }
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        lam[i] = W(RestoWs::XL(NZ) + i);
+        x0[i] = W(RestoWs::XX0(NX, NZ) + i);
+      }
+      fs = W(S + RestoWs::sFS);
+      mu = W(S + RestoWs::sMU);
+      tau = W(S + RestoWs::sTAU);
+      theta_max = W(S + RestoWs::sTHMAX);
+      theta_min = W(S + RestoWs::sTHMIN);
+      dw_last = W(S + RestoWs::sDWLAST);
+      fth = W(S + RestoWs::sFTH);
+      fph = W(S + RestoWs::sFPH);
+      nfilt = (int)W(S + RestoWs::sNFILT);
+      fnext = (int)W(S + RestoWs::sFNEXT);
+      frej = (int)W(S + RestoWs::sFREJ);
+      nfreset = (int)W(S + RestoWs::sNFRESET);
+      acc_count = (int)W(S + RestoWs::sACC);
+      f_last = W(S + RestoWs::sFLAST);
+      soft = W(S + RestoWs::sSOFT) != 0.0;
+      soft_count = (int)W(S + RestoWs::sSOFTN);
+      it = (int)W(S + RestoWs::sIT);
+      step = (int)W(S + RestoWs::sSTEP);
+      warm = W(S + RestoWs::sWARM) != 0.0;
+      if (a.Pseq && step > 0) {  // the step's references (multi-step launches)
+        const double* Pn = a.Pseq + ((size_t)step * a.B + inst) * a.p_stride;
+        Model::load_ctx(ma, inst, Pn, k, hasU, ctx);
+      }
+      scaled = true;
+      pending_rec = true;
+    } else {
+      done = true;
+      step = K - 1;
+    }
+  }
   const long max_pass = (long)K * (a.max_iter + 2);
   for (long pass = 0; pass <= max_pass; ++pass, ++it) {
     if (K > 1) step_boundary();
+    if constexpr (RESUME) {
+      // soft restoration / restoration phase from the state saved at the failed line search
+      // (resto.h); the pass then goes on at the recovered point
+      if (MPCX_COLD(__any(pending_rec))) {
+        if (pending_rec) {
+          pending_rec = false;
+          double* const wsl = a.ws + gid;
+          const long wst = a.ws_stride;
+          auto W = [&](int i) __attribute__((always_inline)) -> double& { return wsl[(long)i * wst]; };
+          constexpr int S = RestoWs::SC(NX, NZ);
+          RecIO io;
+          io.it = (int)W(S + RestoWs::sIT);
+          io.max_iter = a.max_iter;
+          io.k = k;
+          io.N = N;
+          io.nw = nw;
+          io.ng = ng;
+          io.valid = valid;
+          io.hasX = hasX;
+          io.hasU = hasU;
+          io.acc_now = W(S + RestoWs::sACCNOW) != 0.0;
+          io.tol = a.tol;
+          io.mu_min = mu_min;
+          io.fs = fs;
+          io.nbound = nbound;
+          io.thk = W(S + RestoWs::sTHK);
+          io.phk = W(S + RestoWs::sPHK);
+          io.gd = W(S + RestoWs::sGD);
+          io.amax = W(S + RestoWs::sAMAX);
+          io.az = W(S + RestoWs::sAZ);
+          io.sw_a = W(S + RestoWs::sSWA);
+          io.mu = mu;
+          io.tau = tau;
+          io.theta_max = theta_max;
+          io.theta_min = theta_min;
+          io.dw_last = dw_last;
+          io.fth = fth;
+          io.fph = fph;
+          io.nfilt = nfilt;
+          io.fnext = fnext;
+          io.frej = frej;
+          io.nfreset = nfreset;
+          io.soft = soft;
+          io.soft_count = soft_count;
+          io.xslot = xw.slot;
+          recover<Model, G>(io, ma, ctx, wsl, wst, a.lbw, a.ubw, xch);
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) {
+            z[i] = W(RestoWs::XZ + i);
+            zL[i] = W(RestoWs::XZL(NX, NZ) + i);
+            zU[i] = W(RestoWs::XZU(NX, NZ) + i);
+          }
+#pragma unroll
+          for (int i = 0; i < NX; ++i) lam[i] = W(RestoWs::XL(NZ) + i);
+          mu = io.mu;
+          tau = io.tau;
+          theta_max = io.theta_max;
+          theta_min = io.theta_min;
+          dw_last = io.dw_last;
+          fth = io.fth;
+          fph = io.fph;
+          nfilt = io.nfilt;
+          fnext = io.fnext;
+          frej = io.frej;
+          nfreset = io.nfreset;
+          soft = io.soft;
+          soft_count = io.soft_count;
+          xw.slot = io.xslot;
+          if (io.reset_acc) acc_count = 0;
+          tiny_flag = false;
+#ifdef MPCX_STAMPS
+          if (io.it_next > io.it + 1) diag[13] += io.it_next - io.it - 1;  // restoration iterations
+#endif
+          if (io.status >= 0) {
+            done = true;
+            status = io.status;
+            its = io.its;
+          }
+          it = io.it_next;  // this pass is that iteration
+        }
+      }
+    }
     // ------------------------------------------------------------ evaluation
     //  skipped when the line search already evaluated the accepted point; only the groups
     //  that need it evaluate (exec-masked, group-uniform), so an instance's sequence of
@@ -427,7 +586,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     } else {
       sweep();
     }
-    if (it == 0) {
+    if (!scaled) {
+      scaled = true;
       // objective scaling (IPOPT nlp_scaling_method = gradient-based, max_gradient = 100).
       // With lambda scaled by the same factor the Lagrangian's gradient and Hessian scale
       // exactly by fs, so no re-evaluation is needed.
@@ -549,7 +709,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     if (inst == 0 && (k % 64) == 0)
       printf("OPT it=%d k=%d fs=%g Ed=%g Ec=%g E0=%g sd=%g lam1=%g z1=%g\n", it, k, fs, Ed, Ec, E0, sd, lam1, z1);
 #endif
-    if (__all(done && step == K - 1)) break;
+    if (__all((done && step == K - 1) || parked)) break;
     // multi-step launches: a wave whose instances all just finished a step skips the rest of
     // this pass (its Newton step would be discarded) and restarts at the step boundary
     if (K > 1 && __all(done)) continue;
@@ -989,7 +1149,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     const double thk = gsum<G>(thk_l, xw), phk = gsum<G>(phk_l, xw);
     const bool tinystep = tiny < 10.0 * kEps;
     double alpha = amax;
-    bool searching = !done && !tinystep;
+    bool searching = !done && !tinystep && !(kRes && soft);
     bool accepted = !done && tinystep;
     bool ftype = tinystep;
     tiny_flag = !done && tinystep;
@@ -1318,7 +1478,72 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       }
     }
     }
-    if (!done && !accepted) {
+    // ---- soft restoration / restoration phase (resto.h): the failed line search's iterate, its
+    //      Newton step and the loop's scalars go to the workspace; the solve launch parks the
+    //      instance there (the resume launch recovers and continues it), the resume launch
+    //      recovers at the top of its next pass
+    bool handled = false;
+    if constexpr (kRes) {
+      const bool need_rec = res_on && !done && !tinystep && (soft || !accepted);
+      if (MPCX_COLD(__any(need_rec))) {
+        if (need_rec) {
+          DIAG(12);
+          double* const wsl = a.ws + gid;
+          const long wst = a.ws_stride;
+          auto W = [&](int i) __attribute__((always_inline)) -> double& { return wsl[(long)i * wst]; };
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) {
+            W(RestoWs::XZ + i) = z[i];
+            W(RestoWs::XZL(NX, NZ) + i) = zL[i];
+            W(RestoWs::XZU(NX, NZ) + i) = zU[i];
+            W(RestoWs::XDZ(NX, NZ) + i) = dz[i];
+            W(RestoWs::XDZL(NX, NZ) + i) = dzL[i];
+            W(RestoWs::XDZU(NX, NZ) + i) = dzU[i];
+          }
+#pragma unroll
+          for (int i = 0; i < NX; ++i) {
+            W(RestoWs::XL(NZ) + i) = lam[i];
+            W(RestoWs::XDL(NX, NZ) + i) = dlam[i];
+            W(RestoWs::XX0(NX, NZ) + i) = x0[i];
+          }
+          constexpr int S = RestoWs::SC(NX, NZ);
+          W(S + RestoWs::sFS) = fs;
+          W(S + RestoWs::sMU) = mu;
+          W(S + RestoWs::sTAU) = tau;
+          W(S + RestoWs::sTHMAX) = theta_max;
+          W(S + RestoWs::sTHMIN) = theta_min;
+          W(S + RestoWs::sDWLAST) = dw_last;
+          W(S + RestoWs::sFTH) = fth;
+          W(S + RestoWs::sFPH) = fph;
+          W(S + RestoWs::sNFILT) = nfilt;
+          W(S + RestoWs::sFNEXT) = fnext;
+          W(S + RestoWs::sFREJ) = frej;
+          W(S + RestoWs::sNFRESET) = nfreset;
+          W(S + RestoWs::sACC) = acc_count;
+          W(S + RestoWs::sFLAST) = f_last;
+          W(S + RestoWs::sSOFT) = soft ? 1.0 : 0.0;
+          W(S + RestoWs::sSOFTN) = soft_count;
+          W(S + RestoWs::sIT) = it;
+          W(S + RestoWs::sSTEP) = step;
+          W(S + RestoWs::sWARM) = warm ? 1.0 : 0.0;
+          W(S + RestoWs::sTHK) = thk;
+          W(S + RestoWs::sPHK) = phk;
+          W(S + RestoWs::sGD) = gd;
+          W(S + RestoWs::sAMAX) = amax;
+          W(S + RestoWs::sAZ) = az;
+          W(S + RestoWs::sSWA) = sw_a;
+          W(S + RestoWs::sACCNOW) = acceptable_now ? 1.0 : 0.0;
+          if constexpr (RESUME) {
+            pending_rec = true;  // recovered at the top of the next pass
+          } else {
+            W(S + RestoWs::sPEND) = 1.0;  // left to the resume launch
+            done = parked = true;
+          }
+          handled = true;
+        }
+      }
+    }
+    if (!done && !accepted && !handled) {
 #ifdef MPCX_STAMPS
       if (k == 0)
         printf("LSFAIL inst=%d step=%d it=%d mu=%.3e thk=%.6e phk=%.10e gd=%.3e amax=%.3e alpha=%.3e amin=%.3e "
@@ -1333,7 +1558,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 
     STAMP(7);
     // ------------------------------------------------------------ update iterate
-    if (!done) {
+    if (!done && !handled) {
       if (!ftype) {  // augment the filter (entry slot fnext lives on lane fnext)
         if (k == fnext) {
           fth = (1.0 - kGammaTheta) * thk;
@@ -1375,9 +1600,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   }
   STAMP(9);
 #ifdef MPCX_STAMPS
-  if (g_mpcx_diag && valid && k == 0)
+  if (g_mpcx_diag && valid && active && k == 0)
     for (int i = 0; i < kDiag; ++i) g_mpcx_diag[(size_t)inst * kDiag + i] = diag[i];
-  if (g_mpcx_stamps && (threadIdx.x & 63) == 0) {
+  if (g_mpcx_stamps && !RESUME && (threadIdx.x & 63) == 0) {
     const long wv = gid / 64;
     for (int i = 0; i < 10; ++i) g_mpcx_stamps[wv * 10 + i] = st_acc[i];
   }
@@ -1393,7 +1618,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   if (inst == 0 && (k % 64) == 0)
     printf("END k=%d fs=%g mu=%g it=%d lam0=%g z0=%g zL=%g zU=%g\n", k, fs, mu, it, lam[0], z[0], zL[NX], zU[NX]);
 #endif
-  if (valid) {
+  const bool writes = valid && !parked && active;  // parked: the resume launch writes them
+  if (writes) {
     double* w = a.w_out + (size_t)inst * nw;
     if (hasX)
       for (int i = 0; i < NX; ++i) w[ixw<NX, NU>(k, i)] = z[i];
@@ -1429,7 +1655,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
     for (int i = 0; i < NX; ++i) own[NZ + i] = lam[i] / fs;
     group_next<G, NS>(own, nxt, xw);
-    if (valid) {
+    if (writes) {
       const bool lastX = (k == N), lastU = (k == N - 1);
       double* w0n = a.w0_next + (size_t)inst * nw;
       if (hasX)
@@ -1562,6 +1788,25 @@ static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// the resume launch (models with a restoration phase): same grid, the parked groups only
+template <class Model>
+static hipError_t launch_resume_model(const SolveArgs& a, hipStream_t stream) {
+  if constexpr (!RestoOf<Model>::value) {
+    return hipSuccess;
+  } else {
+    const int G = solve_group_size(a.N, a.B, a.n_simd, a.group_policy);
+    const long threads = (long)a.B * G;
+    const int bs = G > 64 ? G : 64;
+    const int blocks = (int)((threads + bs - 1) / bs);
+    if (G == 16) hipLaunchKernelGGL((solve_kernel<Model, 16, true>), dim3(blocks), dim3(64), 0, stream, a);
+    else if (G == 32) hipLaunchKernelGGL((solve_kernel<Model, 32, true>), dim3(blocks), dim3(64), 0, stream, a);
+    else if (G == 64) hipLaunchKernelGGL((solve_kernel<Model, 64, true>), dim3(blocks), dim3(64), 0, stream, a);
+    else if (G == 128) hipLaunchKernelGGL((solve_kernel<Model, 128, true>), dim3(blocks), dim3(128), 0, stream, a);
+    else hipLaunchKernelGGL((solve_kernel<Model, 256, true>), dim3(blocks), dim3(256), 0, stream, a);
+    return hipGetLastError();
+  }
+}
+
 template <class Model>
 static hipError_t launch_plant_model(const SolveArgs& a, const double* U, double* XF, double* QF, hipStream_t stream) {
   hipLaunchKernelGGL((plant_kernel<Model>), dim3((a.B + 255) / 256), dim3(256), 0, stream, a, U, XF, QF);
@@ -1600,6 +1845,7 @@ static hipError_t launch_shift_model(const SolveArgs& a, double* P, const double
 #define MPCX_INSTANTIATE(Model, tag)                                                                        \
   namespace mpcx {                                                                                          \
   hipError_t launch_solve_##tag(const SolveArgs& a, hipStream_t s) { return launch_solve_model<Model>(a, s); } \
+  hipError_t launch_resume_##tag(const SolveArgs& a, hipStream_t s) { return launch_resume_model<Model>(a, s); } \
   hipError_t launch_plant_##tag(const SolveArgs& a, const double* U, double* XF, double* QF, hipStream_t s) {   \
     return launch_plant_model<Model>(a, U, XF, QF, s);                                                      \
   }                                                                                                         \

@@ -32,6 +32,10 @@
 #include "riccati.h"
 #include "solver.h"
 
+#ifndef MPCX_ODE_RESTO
+#define MPCX_ODE_RESTO true
+#endif
+
 namespace mpcx {
 
 using ::cos;  // the double overloads stay visible next to the HD ones below
@@ -266,6 +270,9 @@ struct OdeModel {
   // though lock-step rises 0.47 M -> 2.19 M), the cart-pole (no gain; +14 % per iteration from
   // the extra registers).
   static constexpr bool kSOC = Dyn::kSOC;
+  // IPOPT's soft restoration and feasibility restoration phase (kernels.h; state in the
+  // restoration workspace): the nonlinear models are the ones whose line searches fail
+  static constexpr bool kResto = MPCX_ODE_RESTO;
   static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT && NX <= 5;  // NX = 6: LDS buffer too large
   struct Ctx {
     double zr[NZ];

@@ -94,28 +94,36 @@ inline int solve_group_size(int N, long B, int n_simd, int group_policy) {
     while (G < 64 && B * G * 2 <= 64L * n_simd) G *= 2;
   return G;
 }
-// Restoration-phase workspace (models with kResto), structure of arrays over threads: slot i
-// of thread t at ws[i * ws_stride + t].  Per lane k: p, n, z_p, z_n of the rows of g_{k+1}
-// (the interval k defect), lane 0 also those of g_0; the proximity reference z_R and the bound
-// multipliers at the restoration start; the original filter entry kept in this lane; the
-// iterate saved before a soft-restoration step (restored if the step is rejected).
+// Restoration workspace (models with kResto; resto.h): the solve loop hands its iterate and
+// Newton step to the out-of-line recovery through it and reads the result back.  Structure of
+// arrays over threads: slot i of thread t at ws[i * ws_stride + t].  Per lane: z, lam, zL, zU,
+// dz, dlam, dzL, dzU and x0 (lane 0's initial state).
 struct RestoWs {
-  static constexpr int P = 0;
-  __host__ __device__ static constexpr int N_(int nx) { return nx; }
-  __host__ __device__ static constexpr int ZP(int nx) { return 2 * nx; }
-  __host__ __device__ static constexpr int ZN(int nx) { return 3 * nx; }
-  __host__ __device__ static constexpr int ROW0(int nx) { return 4 * nx; }  // g_0's p, n, z_p, z_n (lane 0)
-  __host__ __device__ static constexpr int ZR(int nx) { return 8 * nx; }
-  __host__ __device__ static constexpr int ZLR(int nx, int nz) { return 8 * nx + nz; }
-  __host__ __device__ static constexpr int ZUR(int nx, int nz) { return 8 * nx + 2 * nz; }
-  __host__ __device__ static constexpr int FIL(int nx, int nz) { return 8 * nx + 3 * nz; }
-  __host__ __device__ static constexpr int SAVE(int nx, int nz) { return 8 * nx + 3 * nz + 2; }  // z, lam, zL, zU
-  __host__ __device__ static constexpr int slots(int nx, int nu) { return SAVE(nx, nx + nu) + 3 * (nx + nu) + nx; }
+  static constexpr int XZ = 0;
+  __host__ __device__ static constexpr int XL(int nz) { return nz; }
+  __host__ __device__ static constexpr int XZL(int nx, int nz) { return nz + nx; }
+  __host__ __device__ static constexpr int XZU(int nx, int nz) { return 2 * nz + nx; }
+  __host__ __device__ static constexpr int XDZ(int nx, int nz) { return 3 * nz + nx; }
+  __host__ __device__ static constexpr int XDL(int nx, int nz) { return 4 * nz + nx; }
+  __host__ __device__ static constexpr int XDZL(int nx, int nz) { return 4 * nz + 2 * nx; }
+  __host__ __device__ static constexpr int XDZU(int nx, int nz) { return 5 * nz + 2 * nx; }
+  __host__ __device__ static constexpr int XX0(int nx, int nz) { return 6 * nz + 2 * nx; }
+  // group scalars of the solve loop at the failed line search (the same value on every lane)
+  enum Scalar {
+    sPEND = 0,  // 1: the fast solve left this instance to the resume launch
+    sFS, sMU, sTAU, sTHMAX, sTHMIN, sDWLAST, sFTH, sFPH, sNFILT, sFNEXT, sFREJ, sNFRESET, sACC, sFLAST,
+    sSOFT, sSOFTN, sIT, sSTEP, sWARM, sTHK, sPHK, sGD, sAMAX, sAZ, sSWA, sACCNOW, kScalars
+  };
+  __host__ __device__ static constexpr int SC(int nx, int nz) { return 6 * nz + 3 * nx; }
+  __host__ __device__ static constexpr int slots(int nx, int nu) { return SC(nx, nx + nu) + kScalars; }
 };
 // doubles of restoration workspace per thread (0: the model has no restoration phase)
 int resto_ws_slots(int model, int nx, int nu);
 
 hipError_t launch_solve(const SolveArgs& a, hipStream_t stream);
+// the resume launch of models with a restoration phase: continues the instances the solve
+// launch left at a failed line search (no-op for the others)
+hipError_t launch_resume(const SolveArgs& a, hipStream_t stream);
 hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X, const double* U, const double* XR,
                            double* J, hipStream_t stream);
 // plant: x+ = F(x0, u) for B instances (stage-0 model of each instance)

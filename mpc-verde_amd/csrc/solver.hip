@@ -96,6 +96,7 @@ int resto_ws_slots(int model, int nx, int nu) {
 // ---- model dispatch (the entry points live in solve_<model>.hip) -------------------
 #define MPCX_DECLARE(tag)                                                                                       \
   hipError_t launch_solve_##tag(const SolveArgs&, hipStream_t);                                                 \
+  hipError_t launch_resume_##tag(const SolveArgs&, hipStream_t);                                                \
   hipError_t launch_plant_##tag(const SolveArgs&, const double*, double*, double*, hipStream_t);                \
   hipError_t launch_constraints_##tag(const SolveArgs&, const double*, double*, hipStream_t);                    \
   hipError_t launch_shift_##tag(const SolveArgs&, double*, const double*, double*, const double*, double*,       \
@@ -123,6 +124,7 @@ MPCX_DECLARE(cartpole)
   } while (0)
 
 hipError_t launch_solve(const SolveArgs& a, hipStream_t stream) { MPCX_DISPATCH(a, launch_solve, a, stream); }
+hipError_t launch_resume(const SolveArgs& a, hipStream_t stream) { MPCX_DISPATCH(a, launch_resume, a, stream); }
 hipError_t launch_plant(const SolveArgs& a, const double* U, double* XF, double* QF, hipStream_t stream) {
   MPCX_DISPATCH(a, launch_plant, a, U, XF, QF, stream);
 }

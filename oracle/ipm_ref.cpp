@@ -264,7 +264,7 @@ typedef struct oracle_opts {
   int32_t max_iter;                   // 3000
   int32_t acceptable_iter;            // 15
   int32_t restoration;                // 1: soft restoration + restoration phase; 0: a failed line search ends the solve
-  int32_t pad;
+  int32_t max_soc;                    // IPOPT max_soc (second-order corrections per line search; IPOPT 4)
 } oracle_opts;
 
 }  // extern "C"
@@ -992,12 +992,14 @@ int solve_one(Inst<Dyn>& I, double* w, double* lam, const oracle_opts& op, int* 
         mu = std::max(mu_min, std::min(kKappaMu * mu, std::pow(mu, kThetaMu)));
         tau = std::max(kTauMin, 1.0 - mu);
         filter.clear();
-        if (resto) set_prox(e, w, mu);
 #ifdef ORACLE_LEGACY_MU
         if (it > 0) break;
 #endif
       }
       tiny_flag = false;
+      // restoration: the proximity weight follows the barrier parameter from here on (the
+      // barrier test above used the one of the iteration's start)
+      if (resto) set_prox(e, w, mu);
     }
     // ---- barrier gradient and primal-dual Sigma (restoration: also the p, n columns)
     for (int i = 0; i < nw; ++i) {
@@ -1243,6 +1245,7 @@ int solve_one(Inst<Dyn>& I, double* w, double* lam, const oracle_opts& op, int* 
       const double amin = gd < 0 ? kGammaAlpha * std::min(kGammaTheta, std::min(kGammaPhi * thk / (-gd),
                                                                                 sw_rhs / std::pow(-gd, kSPhi)))
                                  : kGammaAlpha * kGammaTheta;
+      bool first_trial = true;
       for (;;) {
         double tht, pht;
         trial(alpha, tht, pht);
@@ -1252,13 +1255,66 @@ int solve_one(Inst<Dyn>& I, double* w, double* lam, const oracle_opts& op, int* 
           ftype = ft;
           break;
         }
+        if (first_trial && !resto && op.max_soc > 0 && tht >= thk) {
+          // IPOPT's second-order correction (W&B 2006 A-5.7-A-5.9): the Newton system with the
+          // same matrix for the constraint residual c_soc = alpha c(x_k) + c(x_trial), stepped to
+          // the boundary and tested with the first trial's alpha; accumulated while the
+          // infeasibility shrinks by kappa_soc = 0.99
+          Eval<Dyn> es = e;
+          for (int r = 0; r < ng; ++r) es.c[r] = alpha * e.c[r] + et.c[r];
+          double th_old = thk;
+          std::vector<double> dws, lamS, dzLs(nw), dzUs(nw);
+          for (int ps = 0; ps < op.max_soc; ++ps) {
+            if (!riccati(I, es, sig, gphi, nullptr, delta, RestoRows(), dws, lamS)) break;
+            double as = 1.0, azs = 1.0;
+            for (int i = 0; i < nw; ++i) {
+              dzLs[i] = dzUs[i] = 0;
+              if (I.hasL[i]) {
+                const double sl = w[i] - I.lb[i];
+                dzLs[i] = mu / sl - zL[i] - zL[i] / sl * dws[i];
+                if (dws[i] < 0) as = std::min(as, -tau * sl / dws[i]);
+                if (dzLs[i] < 0) azs = std::min(azs, -tau * zL[i] / dzLs[i]);
+              }
+              if (I.hasU[i]) {
+                const double su = I.ub[i] - w[i];
+                dzUs[i] = mu / su - zU[i] + zU[i] / su * dws[i];
+                if (dws[i] > 0) as = std::min(as, tau * su / dws[i]);
+                if (dzUs[i] < 0) azs = std::min(azs, -tau * zU[i] / dzUs[i]);
+              }
+            }
+            for (int i = 0; i < nw; ++i) wt[i] = w[i] + as * dws[i];
+            evaluate(I, wt.data(), lam, false, et);
+            const double ths = norm1(et.c), phs = et.f - mu * barrier_sum(wt.data());
+            bool fts;
+            if (acceptable(ths, phs, alpha, fts)) {
+              accepted = true;
+              ftype = fts;
+              dw = dws;
+              lamNew = lamS;
+              dzL = dzLs;
+              dzU = dzUs;
+              alpha = as;
+              alpha_d = azs;
+              break;
+            }
+            if (ps == op.max_soc - 1 || ths > 0.99 * th_old) break;
+            for (int r = 0; r < ng; ++r) es.c[r] = as * es.c[r] + et.c[r];
+            th_old = ths;
+          }
+          if (accepted) break;
+        }
+        first_trial = false;
         alpha *= 0.5;
         if (alpha < amin) break;
       }
       if (!accepted) {
         TRACE("it=%d resto=%d line search failed thk=%.3e phk=%.6e gd=%.3e mu=%.2e delta=%.2e E0=%.3e\n", it, (int)resto,
               thk, phk, gd, mu, delta, E0);
-        if (resto || !op.restoration) {
+        if (!resto && !op.restoration) {
+          status = acceptable_now ? kAcceptable : kRestoFailed;
+          break;
+        }
+        if (resto) {
           status = kRestoFailed;
           break;
         }
@@ -1330,15 +1386,19 @@ int solve_one(Inst<Dyn>& I, double* w, double* lam, const oracle_opts& op, int* 
       status = kRestoFailed;
       break;
     }
+    // (a soft-restoration step accepted by the primal-dual error leaves the filter and its
+    //  reset heuristic untouched)
     if (augment && !ftype) filter.emplace_back((1 - kGammaTheta) * thk, phk - kGammaPhi * thk);
-    if (lastrej_f) {  // filter reset heuristic
-      if (++frej >= 5 && nfreset < 5) {
-        filter.clear();
-        ++nfreset;
+    if (augment) {
+      if (lastrej_f) {  // filter reset heuristic
+        if (++frej >= 5 && nfreset < 5) {
+          filter.clear();
+          ++nfreset;
+          frej = 0;
+        }
+      } else {
         frej = 0;
       }
-    } else {
-      frej = 0;
     }
     // ---- update
     for (int i = 0; i < nw; ++i) w[i] += alpha * dw[i];
@@ -1423,7 +1483,7 @@ oracle_opts default_opts(int max_iter, double tol) {
   o.max_iter = max_iter;
   o.acceptable_iter = 15;
   o.restoration = 1;
-  o.pad = 0;
+  o.max_soc = 0;  // the product's unicycle kernel takes no second-order correction
   return o;
 }
 

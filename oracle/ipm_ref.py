@@ -155,14 +155,17 @@ class OracleOpts(ctypes.Structure):
                 ("acceptable_dual_inf_tol", ctypes.c_double), ("acceptable_constr_viol_tol", ctypes.c_double),
                 ("acceptable_compl_inf_tol", ctypes.c_double), ("acceptable_obj_change_tol", ctypes.c_double),
                 ("max_iter", ctypes.c_int32), ("acceptable_iter", ctypes.c_int32), ("restoration", ctypes.c_int32),
-                ("pad", ctypes.c_int32)]
+                ("max_soc", ctypes.c_int32)]
 
 
 # IPOPT defaults (its documented option values)
 IPOPT_DEFAULTS = {"tol": 1e-8, "dual_inf_tol": 1.0, "constr_viol_tol": 1e-4, "compl_inf_tol": 1e-4,
                   "acceptable_tol": 1e-6, "acceptable_dual_inf_tol": 1e10, "acceptable_constr_viol_tol": 1e-2,
                   "acceptable_compl_inf_tol": 1e-2, "acceptable_obj_change_tol": 1e20, "max_iter": 3000,
-                  "acceptable_iter": 15, "restoration": 1}
+                  "acceptable_iter": 15, "restoration": 1, "max_soc": None}
+# the product takes IPOPT's second-order correction (max_soc 4) for the 6-state bicycle only
+# (DESIGN §3.4); max_soc=None follows that per-model choice
+PRODUCT_SOC = {"dyn_bicycle": 4}
 MODEL_IDS = {"unicycle": 1, "kin_bicycle": 3, "dyn_bicycle": 4, "cartpole": 5}
 
 
@@ -204,6 +207,8 @@ def solve(ocp, P, w0=None, lbw=None, ubw=None, lam0=None, lamx0=None, warm=None,
         if k not in o:
             raise ValueError(f"unknown option {k}")
         o[k] = v
+    if o["max_soc"] is None:
+        o["max_soc"] = PRODUCT_SOC.get(getattr(ocp, "model", "unicycle"), 0)
     op = OracleOpts()
     for k, v in o.items():
         setattr(op, k, v)

@@ -366,3 +366,34 @@ def test_scan_fallback_on_indefinite_stage_weights(mpcx, R):
         _, U_ref, J = R.lq_solve(x0[b], lin.A, lin.B, lin.c, lin.W, lin.tab, zr[b], [-1.0], [1.0])
         assert rel(U[b], U_ref[:, 0]) <= 1e-5, b
         assert abs(r["f"][b] - J) <= 1e-7 * max(1.0, abs(J)), b
+
+
+@pytest.mark.parametrize("dec", ["1", "0"])
+def test_pendulum_run_equals_lockstep_decoupled_suffix(mpcx, dec, monkeypatch):
+    """The config-5 path as benchmarked: DeviceLoop.run(K) (one multi-step launch: warm duals,
+    mu_init 1e-4, kb / pcv re-derived at every step boundary, two-wave groups at N = 100) against
+    K lock-step launches, with the decoupled-suffix reuse on and off (MPCX_DEC_SUFFIX=0): the same
+    bits for w, multipliers, iterations and status at every step."""
+    import torch
+    from mpcx import dist as mdist
+    from mpcx import lti
+    from mpcx.device import DeviceLoop
+
+    monkeypatch.setenv("MPCX_DEC_SUFFIX", dec)
+    lin = lti.inverted_pendulum_qp(N=100)
+    S = mpcx.nlpsol("pend", "mi355x", lin, {"ipopt": {"max_iter": 200}})
+    P = lti.pendulum_params(lin, mdist.config5_inputs(0, 64), 0.0)
+    lock, run = DeviceLoop(S, P), DeviceLoop(S, P)
+    st_l, it_l = [], []
+    for _ in range(4):
+        lock.step()
+        torch.cuda.synchronize()
+        st_l.append(lock.status.cpu().numpy().copy())
+        it_l.append(lock.iters.cpu().numpy().copy())
+    st_r, it_r = run.run(4)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st_r.cpu().numpy(), np.array(st_l))
+    np.testing.assert_array_equal(it_r.cpu().numpy(), np.array(it_l))
+    assert np.all(np.array(st_l) == 0)
+    for n in ("P", "w", "w0", "lam", "lamx", "f"):
+        np.testing.assert_array_equal(getattr(run, n).cpu().numpy(), getattr(lock, n).cpu().numpy(), err_msg=n)

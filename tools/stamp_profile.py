@@ -15,7 +15,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["MPCX_LIB"] = os.path.join(ROOT, "mpc-verde_amd", "mpcx", "libmpcx_stamps.so")
+os.environ["MPCX_LIB"] = os.environ.get("MPCX_STAMPS_LIB") or os.path.join(ROOT, "mpc-verde_amd", "mpcx", "libmpcx_stamps.so")
 sys.path.insert(0, os.path.join(ROOT, "mpc-verde_amd"))
 
 import numpy as np  # noqa: E402
