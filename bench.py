@@ -16,10 +16,15 @@ owns B instances; no collective inside the timed region.
 
 Printed JSON (rank 0): value = total solves/s over all ranks; ms_per_step = the
 max-over-ranks wall time per step; ms_per_solve_p50 = median batched solve-call
-latency (HIP events).  `roofline` describes the RK4 + Jacobian sweep kernel
-(rk4_sens, the HBM-streaming kernel of SURVEY.md §8(d)) at B = 2^19, N = 20;
-`cpu_baseline` times the C++ CPU oracle (oracle/ipm_ref.cpp, kind "port") on
-host cores on a bounded sample of the same workload.
+latency (HIP events).  `roofline` describes the kernel that dominates the timed
+region, the fused solve_kernel: useful FP64 flops per launch (PMC FP64
+lane-flops per group-iteration, profiles/r02_solve_kernel_pmc.json, x the
+fraction of lanes that hold a node, x this launch's group-iterations) / the
+launch's HIP-event time / the FP64 vector peak.  `roofline_sweep` describes the
+RK4 + Jacobian sweep kernel (rk4_sens, the HBM-streaming kernel of SURVEY.md
+§8(d)) at B = 2^19, N = 20.  `cpu_baseline` times the C++ CPU oracle
+(oracle/ipm_ref.cpp, kind "port") on every CPU the process may use, on a
+bounded sample of the same workload, next to a 1-thread figure.
 """
 import argparse
 import json
@@ -35,6 +40,10 @@ import numpy as np  # noqa: E402
 
 METRIC = "MPC solves/sec (batched) + ms/solve p50, unicycle N=20 at 1/2/4/8 MI355X"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# FP64 vector (VALU) peak: AMD's MI355X spec, half the FP32 vector peak of 157.3 TF/s
+# (MI355X_MICROARCH.md); the solve kernel issues scalar-per-lane FP64 FMAs, no MFMA
+PEAK_FP64_TFLOPS = 78.6
+SOLVE_PMC = os.path.join("profiles", "r02_solve_kernel_pmc.json")
 SWEEP_BYTES_PER_STAGE = 256  # read x_k,u_k,x_{k+1} (64 B) + write c,q,A,B,grad q (192 B)
 SWEEP_BYTES_PER_INSTANCE = 48  # P
 
@@ -196,6 +205,58 @@ def _cold(P, N, nlp_ref):
     return nlp_ref.join_w(X, np.zeros((P.shape[0], N, 2)))
 
 
+CFG_KERNEL = {2: "UnicycleModel", 3: "UnicycleModel", 4: "LinearModel<4, 1>", 5: "LinearModel<5, 1>"}
+VARIANT_KERNEL = {"kin_bicycle": "KinBicycle", "dyn_bicycle": "DynBicycle", "cartpole": "CartPole"}
+
+
+def group_size(N, B, n_simd, policy=0):
+    """Lanes per instance of the solve launch (csrc/solver.h solve_group_size)."""
+    G = 16 if N < 16 else 32 if N < 32 else 64 if N < 64 else 128 if N < 128 else 256
+    if policy == 0:
+        while G < 64 and B * G * 2 <= 64 * n_simd:
+            G *= 2
+    return G
+
+
+def usable_cpus():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup-v2 CPU quota
+    (the GPU box's share of the host); an inherited OMP_NUM_THREADS is ignored."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(float(quota) / float(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def solve_roofline(kernel_substr, G, n_nodes, group_iters, ms):
+    """Roofline entry of the fused solve kernel from the committed PMC characterisation."""
+    path = os.path.join(ROOT, SOLVE_PMC)
+    if not os.path.exists(path) or ms <= 0 or group_iters <= 0:
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    for k, v in d.items():
+        if kernel_substr in k and f", {G}, false>" in k and v.get("f64_lane_flops_per_group_iteration"):
+            frac_lanes = min(n_nodes, G) / G
+            fl = v["f64_lane_flops_per_group_iteration"] * frac_lanes * group_iters
+            ach = fl / (ms * 1e-3) / 1e12
+            return {"kernel": k, "bound": "valu", "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 4), "traffic": None,
+                    "launch_ms": round(ms, 4), "group_iterations_per_launch": int(group_iters),
+                    "useful_lane_fraction": round(frac_lanes, 4),
+                    "f64_lane_flops_per_group_iteration_all_lanes": v["f64_lane_flops_per_group_iteration"],
+                    "frac_all_lanes": round(ach / frac_lanes / PEAK_FP64_TFLOPS, 4),
+                    "algorithmic_flops_per_launch": fl, "source": SOLVE_PMC,
+                    "note": "FP64 VALU work of the lanes that hold a node (k <= N) only; the kernel is bound "
+                            "by the issue of each instance's serial chains, not by HBM (traffic = its "
+                            "inputs/outputs, see solve_kernel.hbm_frac)"}
+    return None
+
+
 def sweep_roofline(solver, torch, B, N, reps, stream):
     """Time the rk4_sens sweep kernel at B instances (tiled SoA buffers resident in HBM)."""
     from mpcx import _lib
@@ -244,24 +305,6 @@ def load_traffic(B, N):
             d = json.load(f)
         if d.get("B") == B and d.get("N") == N:
             return float(d["hbm_bytes_per_launch"])
-    except Exception:
-        return None
-    return None
-
-
-def load_solve_pmc(kernel_substr):
-    """PMC characterisation of the solve kernel (tools/solve_pmc.sh -> profiles/), if committed."""
-    path = os.path.join(ROOT, "profiles", "r01_solve_kernel_pmc.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        for k, v in d.items():
-            if kernel_substr in k:
-                return {"kernel": k, "wave_cycles_share": v["wave_cycles_share"],
-                        "valu_active_share": v["valu_active_share"], "fp64_tflops": v.get("fp64_tflops"),
-                        "fp64_frac_of_peak": v.get("fp64_frac_of_peak"), "source": "profiles/r01_solve_kernel_pmc.json"}
     except Exception:
         return None
     return None
@@ -354,10 +397,11 @@ def main():
         P0 = mpcx.lti.pendulum_params(ocp, mdist.config5_inputs(start, stop), 0.0)
     loop = DeviceLoop(solver, P0, device=dev, stream=stream)
 
+    warm_it = torch.zeros((max(args.warmup, 1), B), dtype=torch.int32, device=loop.P.device)
     for t in range(args.warmup):
         if per_step is not None:
             per_step(loop, t)
-        loop.step()
+        loop.step(iters_out=warm_it[t])
     torch.cuda.synchronize()
     K = args.steps
     iters_hist = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
@@ -370,10 +414,13 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev_run = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     if args.mode == "async":
         # K closed-loop steps in ONE launch; every instance runs its own receding-horizon loop
         # (bit-identical to K lock-step launches, tests/test_gpu_parity.py::test_run_*)
+        ev_run[0].record(stream)
         loop.run(K, status_out=status_hist, iters_out=iters_hist, Pseq=Pseq, tabseq=tabseq)
+        ev_run[1].record(stream)
     else:
         for i in range(K):
             if per_step is not None and i > 0:
@@ -421,6 +468,9 @@ def main():
     iters_max_step = mdist.max_over_ranks(float(iters_hist.max(dim=1).values.double().mean().item()),
                                           device=loop.P.device)
 
+    # group-iterations of every solve launch of this run (PMC normalisation, tools/solve_pmc_summary.py)
+    iters_all = int(warm_it[:args.warmup].sum().item() + iters_hist.sum().item() + lk_it.sum().item())
+
     roof = None
     if rank == 0 and not args.no_roofline and cfg == 2:
         Br = args.roofline_batch
@@ -433,10 +483,20 @@ def main():
                 "launch_ms": round(ms, 4), "units_per_launch": Br * N, "unit_of_work": "stage evaluation",
                 "bytes_per_launch": alg, "config": f"B={Br}, N={N}"}
 
+    # the dominant kernel of the timed region: the multi-step solve launch (async mode; HIP
+    # events on the launch stream) or the mean single-step launch (lock-step latency run)
+    n_simd = 4 * torch.cuda.get_device_properties(local).multi_processor_count
+    G = group_size(N, B, n_simd, solver.group_policy)
+    if args.mode == "async":
+        run_ms, run_iters = ev_run[0].elapsed_time(ev_run[1]), int(iters_hist.sum().item())
+    else:
+        run_ms, run_iters = float(np.sum(solve_ms)), int(lk_it.sum().item())
+    kname = VARIANT_KERNEL[variant] if variant else CFG_KERNEL[cfg]
+    roof_solve = solve_roofline(kname, G, N + 1, run_iters, run_ms) if rank == 0 else None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and cfg == 2:
-        cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-        cores = max(1, min(cores, os.cpu_count() or 1))
+        cores = usable_cpus()
         make_P = lambda r: mdist.config2_inputs(r * B, (r + 1) * B, args.seed)  # noqa: E731
         rate, t, reps = cpu_baseline(make_P, N, args.warmup + args.steps, cores, min_seconds=args.cpu_seconds)
         # the reference's own loop is one solve at a time on one core (multiple_shooting_casadi.py:226-298)
@@ -450,7 +510,7 @@ def main():
                "value_1core": round(rate1, 1),
                "sample_1core": f"{reps1} x ({args.warmup + args.steps}-step closed loop of {B1} instances), "
                                f"{t1:.1f} s on 1 thread",
-               "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
+               "host_cpus": os.cpu_count(), "usable_cpus": cores, "cpu_model": cpu_model()}
 
     # the kernel that dominates the timed step: the fused solve (+ plant/shift) launch.  Its HBM
     # traffic is its inputs and outputs only, so neither HBM nor the FP64 pipes bound it: it is
@@ -464,8 +524,7 @@ def main():
                   "us_per_ipm_iteration": round(p50 * 1e3 / max(lock_iters_max, 1.0), 2),
                   "hbm_bytes_per_launch": io_bytes,
                   "hbm_frac": round(io_bytes / (p50 * 1e-3) / 1e9 / PEAK_HBM_GBS, 5)}
-    if cfg == 2 and variant is None:
-        solve_info["pmc"] = load_solve_pmc("UnicycleModel")
+    solve_info.update({"group_size": G, "timed_launch_ms": round(run_ms, 4), "timed_group_iterations": run_iters})
     if rank == 0:
         total = world * B * K
         out = {
@@ -485,7 +544,8 @@ def main():
             "iters_mean": round(float(S_all[:, 1].mean()), 2), "iters_max": int(S_all[:, 2].max()),
             "iters_max_per_step_mean": round(float(iters_max_step), 2),
             "failed_instances": int((S_all[:, 3] > 1).sum()),
-            "roofline": roof, "cpu_baseline": cpu, "solve_kernel": solve_info,
+            "iters_sum_all_steps": int(iters_all),
+            "roofline": roof_solve, "roofline_sweep": roof, "cpu_baseline": cpu, "solve_kernel": solve_info,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

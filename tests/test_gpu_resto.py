@@ -11,7 +11,7 @@ restatement (oracle/ipm_ref.cpp) from the same starting points:
 
 PARITY UNPINNED for the ODE models (no reference outputs exist: BASELINE extensions); the oracle
 is an independent restatement of the same algorithm.  Tolerances: inputs 1e-6 relative to
-max(|u|_inf, 1); KKT residual (oracle/ode_ref.py) <= 1e-6.
+max(|u|_inf, 1); KKT residual (oracle/ode_ref.py) <= 1e-6, constraint violation <= tol = 1e-8.
 """
 import numpy as np
 import pytest
@@ -55,7 +55,7 @@ def config4_batch(mpcx, B=1024, N=50):
 
 def certify(pr, r, P, b):
     kkt, gres = pr.kkt_residual(r["w"][b], r["lam_g"][b], r["lam_x"][b], P[b])
-    return kkt <= 1e-6 and gres <= 1e-9, (kkt, gres)
+    return kkt <= 1e-6 and gres <= 1e-8, (kkt, gres)  # tol = 1e-8 (constraint violation)
 
 
 def compare(name, ocp, P, r, ref, nx, nz, max_differ, max_iter_differ):
@@ -87,7 +87,7 @@ def test_config4_dyn_bicycle_batch_vs_ipopt_oracle(mpcx, C):
     r = solver.solve_batch(P)
     ref = C.solve(ocp, P, nthreads=0)
     compare("config 4 dyn bicycle N=50", ocp, P, r, ref, 6, 8, max_differ=8, max_iter_differ=120)
-    assert np.min(r["w"][:, 6 + 3::8]) >= 2.5  # the vx >= 2.5 bound holds (X_1..X_N)
+    assert np.min(r["w"][:, 6 + 2 + 3::8]) >= 2.5 - 1e-7  # vx >= 2.5 holds on X_1..X_N (stage k: U_k, X_k+1)
 
 
 def test_config5_single_shooting_swingup_N100(mpcx, C):

@@ -15,7 +15,7 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
   SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d "$OUT/a" -o pmc -- python3 "$R/bench.py" "${ARGS[@]}" \
   > "$OUT/a.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 \
-  SQ_INSTS_VALU_TRANS_F64 GRBM_GUI_ACTIVE --output-format csv -d "$OUT/b" -o pmc -- python3 "$R/bench.py" "${ARGS[@]}" \
+  SQ_INSTS_VALU_TRANS_F64 --output-format csv -d "$OUT/b" -o pmc -- python3 "$R/bench.py" "${ARGS[@]}" \
   > "$OUT/b.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace -- \
   python3 "$R/bench.py" "${ARGS[@]}" > "$OUT/trace.log" 2>&1

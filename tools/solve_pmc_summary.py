@@ -1,11 +1,15 @@
 """Summarise tools/solve_pmc.sh: per-dispatch averages over the solve_kernel dispatches.
 
-    python tools/solve_pmc_summary.py gpurun_out/solve_pmc > profiles/r01_solve_kernel_pmc.json
+    python tools/solve_pmc_summary.py gpurun_out/solve_pmc > profiles/r02_solve_kernel_pmc.json
 
 SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles summed over waves
 (MI355X_MICROARCH.md, PMC units); WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES.
 FP64 lane-operations = 64 x (ADD + MUL + TRANS + 2 FMA) wave-instructions (inactive lanes
 included: an upper bound on useful flops).  Peak FP64 vector: 78.6 TFLOP/s (MI355X spec).
+f64_lane_flops_per_group_iteration = the kernel's lane-flops summed over its dispatches / the
+IPM iterations of all lane groups in the run (bench.py's `iters_sum_all_steps`, read from the
+pass-B log): bench.py scales it by the fraction of lanes holding a node and by a launch's
+group-iterations for its live roofline entry.
 """
 import csv
 import glob
@@ -27,7 +31,19 @@ def counters(d):
                 continue
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[k].add(r["Dispatch_Id"])
-    return {k: {c: v / len(disp[k]) for c, v in cs.items()} | {"dispatches": len(disp[k])} for k, cs in agg.items()}
+    return {k: {c: v / len(disp[k]) for c, v in cs.items()} | {"dispatches": len(disp[k]), "_total": dict(cs)}
+            for k, cs in agg.items()}
+
+
+def bench_iters(log):
+    """iters_sum_all_steps of the bench JSON line in a pass log."""
+    try:
+        for line in open(log):
+            if line.startswith("{") and "iters_sum_all_steps" in line:
+                return json.loads(line)["iters_sum_all_steps"]
+    except OSError:
+        pass
+    return None
 
 
 def durations(d):
@@ -50,6 +66,10 @@ def main():
         wc = ca["SQ_WAVE_CYCLES"]
         f64 = {n: cb.get(f"SQ_INSTS_VALU_{n}_F64", 0.0) for n in ("ADD", "MUL", "FMA", "TRANS")}
         flops = 64 * (f64["ADD"] + f64["MUL"] + f64["TRANS"] + 2 * f64["FMA"])
+        tot = cb.get("_total", {})
+        flops_total = 64 * sum((2 if n == "FMA" else 1) * tot.get(f"SQ_INSTS_VALU_{n}_F64", 0.0)
+                               for n in ("ADD", "MUL", "FMA", "TRANS"))
+        its = bench_iters(os.path.join(root, "b.log"))
         r = {"dispatches": ca["dispatches"], "duration_ms_median": None if t is None else round(t * 1e3, 4),
              "wave_cycles_share": {"issuing": round(ca["SQ_ACTIVE_INST_ANY"] / wc, 4),
                                    "dependency_or_pipe_stall": round(ca["SQ_WAIT_INST_ANY"] / wc, 4),
@@ -57,7 +77,9 @@ def main():
              "valu_active_share": round(ca["SQ_ACTIVE_INST_VALU"] / wc, 4),
              "insts_per_dispatch": {"valu": ca["SQ_INSTS_VALU"], "salu": ca["SQ_INSTS_SALU"], "lds": ca["SQ_INSTS_LDS"]},
              "f64_insts_per_dispatch": f64, "f64_lane_flops_per_dispatch": flops,
-             "valu_f64_share_of_valu": round(sum(f64.values()) / max(ca["SQ_INSTS_VALU"], 1.0), 4)}
+             "valu_f64_share_of_valu": round(sum(f64.values()) / max(ca["SQ_INSTS_VALU"], 1.0), 4),
+             "group_iterations_in_run": its,
+             "f64_lane_flops_per_group_iteration": (flops_total / its) if its and ", true>" not in k else None}
         if t:
             r["fp64_tflops"] = round(flops / t / 1e12, 3)
             r["fp64_frac_of_peak"] = round(flops / t / 1e12 / PEAK_FP64_TFLOPS, 4)
