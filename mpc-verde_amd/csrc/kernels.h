@@ -39,7 +39,7 @@
 static __device__ unsigned long long* g_mpcx_stamps = nullptr;
 // per-instance event counters (diagnostic build; indices at the kernel's `diag` array)
 static __device__ int* g_mpcx_diag = nullptr;
-constexpr int kDiag = 14;  // counters per instance
+constexpr int kDiag = 15;  // counters per instance
 #define DIAG(i) (++diag[(i)])
 #define DIAG_IF(c, i) \
   do {                \
@@ -118,6 +118,77 @@ __device__ __forceinline__ double barrier_logsum(const double* z, const double* 
   }
   return log(m) + (double)e * 0.69314718055994530942;
 }
+
+// IPOPT's filter (W&B 2006 §2.4, Filter::AddEntry) held in LDS by the lanes of a group: lane k
+// owns entry slots k + G j, j < S = FilterLds<G>::S (S G >= 256 entries per instance); a free
+// slot holds (+inf, +inf), so the membership test is plain `th >= th_j && ph >= ph_j`.  Entries
+// are appended (slot n, no group collective) until all S G slots have been used; from then on an
+// addition first drops the entries the new one dominates (as IPOPT's AddEntry does; a dominated
+// entry never decides a test, so dropping it earlier would change nothing) and takes the lowest
+// free slot, so the slots bound the filter only when more than S G entries are mutually
+// non-dominated: then slot `next` (rotating) is overwritten and add() returns true (counted by
+// the diagnostic build: DIAG 14).  Tests and updates touch the used rows only (one row while the
+// filter holds at most G entries).  LDS rather than registers: the filter is read once per
+// line-search trial and written once per iteration, and registers are the kernel's bottleneck.
+template <int G>
+struct FilterLds {
+  static constexpr int kB = G > 64 ? G : 64;           // threads per block = column stride
+  static constexpr int S = 256 / G > 2 ? 256 / G : 2;  // slot rows
+  static constexpr int kCap = S * G;
+  static constexpr int kDoubles = 2 * S * kB;          // LDS per block
+  double* p;  // this thread's column of the block's buffer: th_j = p[2 j kB], ph_j = p[(2 j + 1) kB]
+  int n;      // slots used (group-uniform); kCap once the filter has filled up
+  int next;   // overflow slot (rotating)
+  __device__ __forceinline__ double& th(int j) const { return p[(2 * j) * kB]; }
+  __device__ __forceinline__ double& ph(int j) const { return p[(2 * j + 1) * kB]; }
+  __device__ __forceinline__ int rows() const { return (n + G - 1) / G; }
+  __device__ __forceinline__ void clear() {
+    for (int j = 0; j < rows(); ++j) th(j) = ph(j) = INFINITY;
+    n = next = 0;
+  }
+  __device__ __forceinline__ void init(double* col) {  // every slot (kernel start)
+    p = col;
+    n = kCap;
+    clear();
+  }
+  // (t, q) lies in the region of one of this lane's entries
+  __device__ __forceinline__ bool covers(double t, double q) const {
+    bool r = false;
+    for (int j = 0; j < rows(); ++j) r |= t >= th(j) && q >= ph(j);
+    return r;
+  }
+  __device__ __forceinline__ bool contains(double t, double q, XWave<G>& xw) const {
+    return n > 0 && gmax<G>(covers(t, q) ? 1.0 : 0.0, xw) > 0.5;
+  }
+  __device__ __forceinline__ bool add(double nth, double nph, int k, XWave<G>& xw) {
+    if (n < kCap) {  // append
+      if (n % G == k) {
+        th(n / G) = nth;
+        ph(n / G) = nph;
+      }
+      ++n;
+      return false;
+    }
+    // full: drop what the new entry dominates, take the lowest free slot
+    double low = (double)kCap;
+    for (int j = 0; j < S; ++j)
+      if (th(j) >= nth && ph(j) >= nph) {
+        th(j) = ph(j) = INFINITY;
+        low = fmin(low, (double)(k + G * j));
+      }
+    const int slot = (int)gmin<G>(low, xw);
+    const bool ovf = slot >= kCap;
+    const int put = ovf ? next : slot;
+    if (put % G == k) {
+      th(put / G) = nth;
+      ph(put / G) = nph;
+    }
+    if (ovf) next = next + 1 == kCap ? 0 : next + 1;
+    return ovf;
+  }
+};
+static_assert(FilterLds<16>::S <= RestoWs::kFilterMax, "workspace slots of the filter");
+
 
 }  // namespace mpcx
 #include "resto.h"  // IPOPT's soft restoration and restoration phase (cold, out of line)
@@ -312,8 +383,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   const double mu_min = a.tol / 10.0;
   double theta_max = 0.0, theta_min = 0.0;  // set at the first iterate
   double dw_last = 0.0;
-  double fth = 0, fph = 0;  // filter entry #k of my instance (a ring of G entries in the lanes)
-  int nfilt = 0, fnext = 0;
+  __shared__ double fbuf[FilterLds<G>::kDoubles];  // the instances' filters (FilterLds)
+  FilterLds<G> filt;
+  filt.init(fbuf + threadIdx.x);
   // IPOPT's filter-reset heuristic: iterations in a row whose last rejected trial point was
   // rejected by the filter alone, and resets so far in this solve
   int frej = 0, nfreset = 0;
@@ -350,7 +422,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   // 7 f-type (Armijo) acceptances, 8 factorisations by the sequential fallback of the scan,
   // 9 filter resets, 10 first trials rejected with increased infeasibility (SOC-eligible),
   // 11 accepted second-order corrections, 12 recoveries (soft restoration / restoration phase
-  // calls, resto.h), 13 restoration-phase iterations
+  // calls, resto.h), 13 restoration-phase iterations, 14 filter additions that found all G
+  // slots holding mutually non-dominated entries (filter_add; an entry was overwritten)
   int diag[kDiag] = {};
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = 0;
@@ -416,7 +489,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       fs = 1.0;
       theta_max = theta_min = 0.0;
       dw_last = 0.0;
-      nfilt = fnext = 0;
+      filt.clear();
       frej = nfreset = 0;
       acc_count = 0;
       f_last = -1e50;
@@ -465,10 +538,13 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       theta_max = W(S + RestoWs::sTHMAX);
       theta_min = W(S + RestoWs::sTHMIN);
       dw_last = W(S + RestoWs::sDWLAST);
-      fth = W(S + RestoWs::sFTH);
-      fph = W(S + RestoWs::sFPH);
-      nfilt = (int)W(S + RestoWs::sNFILT);
-      fnext = (int)W(S + RestoWs::sFNEXT);
+#pragma unroll
+      for (int j = 0; j < FilterLds<G>::S; ++j) {
+        filt.th(j) = W(S + RestoWs::sFTH + j);
+        filt.ph(j) = W(S + RestoWs::sFPH + j);
+      }
+      filt.next = (int)W(S + RestoWs::sFNEXT);
+      filt.n = (int)W(S + RestoWs::sFN);
       frej = (int)W(S + RestoWs::sFREJ);
       nfreset = (int)W(S + RestoWs::sNFRESET);
       acc_count = (int)W(S + RestoWs::sACC);
@@ -528,16 +604,13 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           io.theta_max = theta_max;
           io.theta_min = theta_min;
           io.dw_last = dw_last;
-          io.fth = fth;
-          io.fph = fph;
-          io.nfilt = nfilt;
-          io.fnext = fnext;
           io.frej = frej;
           io.nfreset = nfreset;
           io.soft = soft;
           io.soft_count = soft_count;
           io.xslot = xw.slot;
-          recover<Model, G>(io, ma, ctx, wsl, wst, a.lbw, a.ubw, xch);
+          io.fovf = 0;
+          recover<Model, G>(io, filt, ma, ctx, wsl, wst, a.lbw, a.ubw, xch);
 #pragma unroll
           for (int i = 0; i < NZ; ++i) {
             z[i] = W(RestoWs::XZ + i);
@@ -551,10 +624,6 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           theta_max = io.theta_max;
           theta_min = io.theta_min;
           dw_last = io.dw_last;
-          fth = io.fth;
-          fph = io.fph;
-          nfilt = io.nfilt;
-          fnext = io.fnext;
           frej = io.frej;
           nfreset = io.nfreset;
           soft = io.soft;
@@ -564,6 +633,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           tiny_flag = false;
 #ifdef MPCX_STAMPS
           if (io.it_next > io.it + 1) diag[13] += io.it_next - io.it - 1;  // restoration iterations
+          diag[14] += io.fovf;
 #endif
           if (io.status >= 0) {
             done = true;
@@ -733,8 +803,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         static_assert(kThetaMu == 1.5, "mu^theta_mu evaluated as mu * sqrt(mu)");
         mu = fmax(mu_min, fmin(kKappaMu * mu, mu * sqrt(mu)));
         tau = fmax(kTauMin, 1.0 - mu);
-        nfilt = 0;
-        fnext = 0;
+        filt.clear();
       }
       if (!__any(dec)) break;
     }
@@ -1195,8 +1264,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       }
       pht_l -= mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU);
       const double tht = gsum<G>(tht_l, xw), pht = gsum<G>(pht_l, xw);
-      const double inF = (k < nfilt && tht >= fth && pht >= fph) ? 1.0 : 0.0;
-      const bool infilter = gmax<G>(inF, xw) > 0.5;
+      const bool infilter = filt.contains(tht, pht, xw);
       if (searching) {
         // sufficient decrease (switching condition + Armijo, or theta/phi decrease), then the
         // filter -- IPOPT's order, which decides whether a rejection was the filter's
@@ -1257,8 +1325,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       pht_l -= mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU);
       tht = gsum<G>(tht_l, xw);
       pht = gsum<G>(pht_l, xw);
-      const double inF = (k < nfilt && tht >= fth && pht >= fph) ? 1.0 : 0.0;
-      infilter = gmax<G>(inF, xw) > 0.5;
+      infilter = filt.contains(tht, pht, xw);
     };
     // acceptance of a trial point for step length al (W&B 2006 A-5.4): sufficient decrease
     // (switching condition + Armijo, or theta/phi decrease), then the filter -- IPOPT's order,
@@ -1437,8 +1504,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
             trial_value(zs, ths, phs, infs, cts, cts0);
 #ifdef MPCX_DEBUG_PRINT
             if (inst == 0 && k == 0)
-              printf("SOC it=%d ps=%d son=%d alpha0=%g as=%g thk=%.17g phk=%.17g ths=%.17g phs=%.17g infs=%d nfilt=%d\n", it,
-                     ps, (int)son, alpha, as, thk, phk, ths, phs, (int)infs, nfilt);
+              printf("SOC it=%d ps=%d son=%d alpha0=%g as=%g thk=%.17g phk=%.17g ths=%.17g phs=%.17g infs=%d fnext=%d\n", it,
+                     ps, (int)son, alpha, as, thk, phk, ths, phs, (int)infs, filt.next);
 #endif
             if (son) {
               bool ft;
@@ -1513,10 +1580,13 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           W(S + RestoWs::sTHMAX) = theta_max;
           W(S + RestoWs::sTHMIN) = theta_min;
           W(S + RestoWs::sDWLAST) = dw_last;
-          W(S + RestoWs::sFTH) = fth;
-          W(S + RestoWs::sFPH) = fph;
-          W(S + RestoWs::sNFILT) = nfilt;
-          W(S + RestoWs::sFNEXT) = fnext;
+#pragma unroll
+          for (int j = 0; j < FilterLds<G>::S; ++j) {
+            W(S + RestoWs::sFTH + j) = filt.th(j);
+            W(S + RestoWs::sFPH + j) = filt.ph(j);
+          }
+          W(S + RestoWs::sFNEXT) = filt.next;
+          W(S + RestoWs::sFN) = filt.n;
           W(S + RestoWs::sFREJ) = frej;
           W(S + RestoWs::sNFRESET) = nfreset;
           W(S + RestoWs::sACC) = acc_count;
@@ -1559,19 +1629,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     STAMP(7);
     // ------------------------------------------------------------ update iterate
     if (!done && !handled) {
-      if (!ftype) {  // augment the filter (entry slot fnext lives on lane fnext)
-        if (k == fnext) {
-          fth = (1.0 - kGammaTheta) * thk;
-          fph = phk - kGammaPhi * thk;
-        }
-        fnext = (fnext + 1) & (G - 1);
-        nfilt = nfilt < G ? nfilt + 1 : G;
+      if (!ftype) {  // augment the filter
+        if (filt.add((1.0 - kGammaTheta) * thk, phk - kGammaPhi * thk, k, xw)) DIAG(14);
       }
       // filter reset (IPOPT filter_reset_trigger = 5, max_filter_resets = 5): the filter is
       // cleared once the last rejection of 5 successive iterations was the filter's
       if (lastrej_f) {
         if (++frej >= kFilterResetTrigger && nfreset < kMaxFilterResets) {
-          nfilt = fnext = 0;
+          filt.clear();
           ++nfreset;
           frej = 0;
           DIAG(9);

@@ -138,16 +138,16 @@ __device__ __forceinline__ bool resto_transform(const double* D, double* P, doub
   return ok;
 }
 
-// Scalars handed between the solve loop and recover() (group-uniform values, except this lane's
-// own filter entry fth, fph).  The arrays travel through the workspace (RestoWs).
+// Scalars handed between the solve loop and recover() (group-uniform values); the filter is
+// passed by reference, the arrays travel through the workspace (RestoWs).
 struct RecIO {
   // in
   int it, max_iter, k, N, nw, ng;
   bool valid, hasX, hasU, acc_now;
   double tol, mu_min, fs, nbound, thk, phk, gd, amax, az, sw_a;
   // in / out
-  double mu, tau, theta_max, theta_min, dw_last, fth, fph;
-  int nfilt, fnext, frej, nfreset, soft_count, xslot;
+  double mu, tau, theta_max, theta_min, dw_last;
+  int frej, nfreset, soft_count, xslot, fovf;  // fovf: filter overflows (FilterLds::add)
   bool soft;
   // out
   int status;   // -1: the solve goes on from the state written back; else the final IPOPT status
@@ -157,8 +157,9 @@ struct RecIO {
 };
 
 template <class Model, int G>
-__device__ MPCX_RECOVER_INLINE void recover(RecIO& io, const ModelArgs ma, const typename Model::Ctx ctx, double* wsl,
-                                     const long wst, const double* lbw, const double* ubw, double* xbuf) {
+__device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const ModelArgs ma,
+                                             const typename Model::Ctx ctx, double* wsl, const long wst,
+                                             const double* lbw, const double* ubw, double* xbuf) {
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2, NP = NX * (NX + 1) / 2;
   const int k = io.k, N = io.N, lane = threadIdx.x & 63;
   const bool valid = io.valid, hasX = io.hasX, hasU = io.hasU, has0 = valid && k == 0;
@@ -322,10 +323,10 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, const ModelArgs ma, const
     }
   };
   // the filter-reset heuristic after an accepted step
-  auto filter_reset = [&](bool lastrej_f, int& nfilt_, int& fnext_) __attribute__((always_inline)) {
+  auto filter_reset = [&](bool lastrej_f, FilterLds<G>& f) __attribute__((always_inline)) {
     if (lastrej_f) {
       if (++io.frej >= kFilterResetTrigger && io.nfreset < kMaxFilterResets) {
-        nfilt_ = fnext_ = 0;
+        f.clear();
         ++io.nfreset;
         io.frej = 0;
       }
@@ -354,8 +355,7 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, const ModelArgs ma, const
     for (int i = 0; i < NX; ++i) tht_l += fabs(c1t[i]) + fabs(c0t[i]);
     const double tht = gsum<G>(tht_l, xw);
     const double pht = gsum<G>(fs * qt - mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU), xw);
-    const double inF = (k < io.nfilt && tht >= io.fth && pht >= io.fph) ? 1.0 : 0.0;
-    const bool infilter = gmax<G>(inF, xw) > 0.5;
+    const bool infilter = filt.contains(tht, pht, xw);
     const double thk = io.thk, phk = io.phk, gd = io.gd;
     bool acc = isfinite(pht) && isfinite(tht) && tht <= io.theta_max, ft = false, lastrej_f = false;
     if (acc) {
@@ -371,15 +371,8 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, const ModelArgs ma, const
       lastrej_f = true;
     }
     if (acc) {  // the original criteria hold: a regular step, and the soft phase ends
-      if (!ft) {
-        if (k == io.fnext) {
-          io.fth = (1.0 - kGammaTheta) * thk;
-          io.fph = phk - kGammaPhi * thk;
-        }
-        io.fnext = (io.fnext + 1) & (G - 1);
-        io.nfilt = io.nfilt < G ? io.nfilt + 1 : G;
-      }
-      filter_reset(lastrej_f, io.nfilt, io.fnext);
+      if (!ft) io.fovf += filt.add((1.0 - kGammaTheta) * thk, phk - kGammaPhi * thk, k, xw);
+      filter_reset(lastrej_f, filt);
 #pragma unroll
       for (int i = 0; i < NZ; ++i) {
         z[i] = zt[i];
@@ -428,12 +421,7 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, const ModelArgs ma, const
   }
   // ======================================================= 3. restoration phase
   // original problem: augment its filter with the current (theta, phi) and keep it
-  if (k == io.fnext) {
-    io.fth = (1.0 - kGammaTheta) * io.thk;
-    io.fph = io.phk - kGammaPhi * io.thk;
-  }
-  io.fnext = (io.fnext + 1) & (G - 1);
-  io.nfilt = io.nfilt < G ? io.nfilt + 1 : G;
+  io.fovf += filt.add((1.0 - kGammaTheta) * io.thk, io.phk - kGammaPhi * io.thk, k, xw);
   const double th_R0 = io.thk, ph_R0 = io.phk, mu_o = mu;
   // proximity reference and scaling, bound multipliers at the start
   double zR[NZ], dr2[NZ], zLR[NZ], zUR[NZ];
@@ -479,8 +467,9 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, const ModelArgs ma, const
   }
 #pragma unroll
   for (int i = 0; i < NX; ++i) lam[i] = 0.0;
-  double rth = 0, rph = 0;  // the restoration problem's filter (a ring of G entries in the lanes)
-  int rnfilt = 0, rfnext = 0;
+  __shared__ double rfbuf[FilterLds<G>::kDoubles];  // the restoration problem's filters
+  FilterLds<G> rfilt;
+  rfilt.init(rfbuf + threadIdx.x);
   double dw_last = 0.0;
   bool tiny_flag = false;
   int steps = 0, itr = io.it;
@@ -527,9 +516,8 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, const ModelArgs ma, const
       for (int i = 0; i < NX; ++i) t += fabs(cdef[i]) + fabs(c0[i]);
       const double th_o = gsum<G>(t, xw);
       const double ph_o = gsum<G>(fs * qv - mu_o * barrier_logsum<NZ>(z, lb, ub, hL, hU), xw);
-      // (io.fth / io.fph / io.nfilt hold the original filter, augmented at the start)
-      const double inF = (k < io.nfilt && th_o >= io.fth && ph_o >= io.fph) ? 1.0 : 0.0;
-      const bool infilter = gmax<G>(inF, xw) > 0.5;
+      // (filt holds the original filter, augmented at the start)
+      const bool infilter = filt.contains(th_o, ph_o, xw);
       if (th_o <= kKappaResto * th_R0 && !infilter &&
           (th_o <= (1.0 - kGammaTheta) * th_R0 || ph_o <= ph_R0 - kGammaPhi * th_R0))
         break;
@@ -599,7 +587,7 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, const ModelArgs ma, const
       if (!((Emu <= kKappaEps * mu || (tiny_flag && rep == 0)) && mu > io.mu_min)) break;
       mu = fmax(io.mu_min, fmin(kKappaMu * mu, mu * sqrt(mu)));
       tau = fmax(kTauMin, 1.0 - mu);
-      rnfilt = rfnext = 0;
+      rfilt.clear();
     }
     tiny_flag = false;
     // ---- barrier gradient, Sigma; the proximity term at the new mu
@@ -888,8 +876,7 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, const ModelArgs ma, const
         for (int i = 0; i < NZ; ++i) zt[i] = fma(alpha, dz[i], z[i]);
         value_c(zt, c1t, c0t, qt);
         resto_theta_phi(zt, alpha, c1t, c0t, eta_n, tht, pht);
-        const double inF = (k < rnfilt && tht >= rth && pht >= rph) ? 1.0 : 0.0;
-        const bool infilter = gmax<G>(inF, xw) > 0.5;
+        const bool infilter = rfilt.contains(tht, pht, xw);
         bool acc = isfinite(pht) && isfinite(tht) && tht <= r_thmax, ft = false;
         if (acc) {
           if (thk <= r_thmin && gd < 0 && alpha > sw_a) {
@@ -921,15 +908,8 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, const ModelArgs ma, const
       return;
     }
     // ---- update
-    if (!ftype) {
-      if (k == rfnext) {
-        rth = (1.0 - kGammaTheta) * thk;
-        rph = phk - kGammaPhi * thk;
-      }
-      rfnext = (rfnext + 1) & (G - 1);
-      rnfilt = rnfilt < G ? rnfilt + 1 : G;
-    }
-    filter_reset(lastrej_f, rnfilt, rfnext);
+    if (!ftype) io.fovf += rfilt.add((1.0 - kGammaTheta) * thk, phk - kGammaPhi * thk, k, xw);
+    filter_reset(lastrej_f, rfilt);
 #pragma unroll
     for (int i = 0; i < NZ; ++i) {
       z[i] = fma(alpha, dz[i], z[i]);

@@ -111,9 +111,12 @@ struct RestoWs {
   // group scalars of the solve loop at the failed line search (the same value on every lane)
   enum Scalar {
     sPEND = 0,  // 1: the fast solve left this instance to the resume launch
-    sFS, sMU, sTAU, sTHMAX, sTHMIN, sDWLAST, sFTH, sFPH, sNFILT, sFNEXT, sFREJ, sNFRESET, sACC, sFLAST,
-    sSOFT, sSOFTN, sIT, sSTEP, sWARM, sTHK, sPHK, sGD, sAMAX, sAZ, sSWA, sACCNOW, kScalars
+    sFS, sMU, sTAU, sTHMAX, sTHMIN, sDWLAST, sFNEXT, sFN, sFREJ, sNFRESET, sACC, sFLAST,
+    sSOFT, sSOFTN, sIT, sSTEP, sWARM, sTHK, sPHK, sGD, sAMAX, sAZ, sSWA, sACCNOW,
+    sFTH,                                      // this lane's filter slots (FilterLds<G>::S of kFilterMax)
+    sFPH = sFTH + 16, kScalars = sFPH + 16
   };
+  static constexpr int kFilterMax = 16;
   __host__ __device__ static constexpr int SC(int nx, int nz) { return 6 * nz + 3 * nx; }
   __host__ __device__ static constexpr int slots(int nx, int nu) { return SC(nx, nx + nu) + kScalars; }
 };

@@ -22,7 +22,8 @@ from mpcx import dist as mdist  # noqa: E402
 from mpcx.device import DeviceLoop  # noqa: E402
 
 NAMES = ["regularised_iters", "extra_factorisations", "backtracks", "barrier_updates", "ftb_limited_steps",
-         "tiny_steps", "filter_rejections", "armijo_acceptances", "scan_fallbacks", "filter_resets", "soc_eligible", "soc_accepted", "soft_resto_steps", "resto_phases"]
+         "tiny_steps", "filter_rejections", "armijo_acceptances", "scan_fallbacks", "filter_resets", "soc_eligible", "soc_accepted", "soft_resto_steps", "resto_phases",
+         "filter_overflows"]
 ND = len(NAMES)  # counters per instance (solver.hip kDiag)
 
 
