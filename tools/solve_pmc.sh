@@ -6,7 +6,7 @@
 # -> gpurun_out/solve_pmc/{a,b,trace}, summarised by tools/solve_pmc_summary.py
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/solve_pmc
+OUT=${SOLVE_PMC_OUT:-$R/gpurun_out/solve_pmc}
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
