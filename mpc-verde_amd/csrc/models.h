@@ -69,6 +69,14 @@ struct UnicycleModel {
   }
 };
 
+// The same model with the backward Riccati recursion as a log-depth scan (pscan.h).  The scan's
+// cost is ceil(log2(N+1)) combine levels whatever N is, the sequential chain's is N steps, so the
+// launch picks this instantiation for longer horizons (solver.hip kUnicycleScanMinN; A/B on one
+// MI355X: config 3, N = 30, +6.5 % solves/s; config 2, N = 20, -4 %).
+struct UnicycleScanModel : UnicycleModel {
+  static constexpr bool kParallelRiccati = true;
+};
+
 // ------------------------------------------------------------------------------------
 // Linear (time-varying) model with quadratic stage cost -- the mpctools LTI/LTV QPs
 // (Inverted_pendulum/inverted_pendulum_single_shooting_mpctools.py:19-64,
