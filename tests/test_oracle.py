@@ -195,3 +195,33 @@ def test_mpctools_variant_reproduces_3exemplo(golden):
     assert max(steps) <= 1e-6
     assert np.abs(xs - rows[:, 0:3]).max() <= 5e-5
     np.testing.assert_allclose(rows[:, 5], 0.2 * np.arange(rows.shape[0]), atol=1e-12)
+
+
+def test_cpp_oracle_restoration_phase_recovers_failed_line_searches():
+    """The C++ IPOPT restatement's soft restoration + restoration phase (W&B 2006 §3.3) on the
+    cold-start instances of configs 4 (6-state bicycle) and 5 (swing-up) whose filter line
+    search fails: without restoration each ends with status 3 at the recorded iteration; with it
+    each converges (status 0) in the recorded number of iterations (the kernel takes the same
+    counts on the swing-up, tests/test_gpu_resto.py) to a KKT point of the NLP."""
+    import mpcx
+    from mpcx import dist as mdist
+    from oracle import ode_ref
+
+    ipm_ref.lib()
+    t0, x0, (X, Y, V) = mdist.config4_bicycle_inputs(0, 1024)
+    ocp4 = mpcx.dynamic_bicycle_lane_change(N=50)
+    idx4 = [262, 483, 10]
+    refs = np.stack([mpcx.ode.dyn_bicycle_references(X, Y, V, int(t0[b]), 50).reshape(-1) for b in idx4])
+    P4 = ocp4.params(x0[idx4], refs)
+    ocp5 = mpcx.cartpole_swingup(N=100)
+    idx5 = [313, 12, 74, 396]
+    P5 = mdist.config5_swingup_inputs(0, 2048)[idx5]
+    for ocp, P, fail_at, iters in ((ocp4, P4, [28, 30, 33], [54, 75, 84]), (ocp5, P5, [8, 7, 8, 16], [22, 21, 20, 35])):
+        off = ipm_ref.solve(ocp, P, restoration=0, max_iter=3000)
+        assert off["status"].tolist() == [3] * len(P) and off["iters"].tolist() == fail_at, (off["status"], off["iters"])
+        on = ipm_ref.solve(ocp, P, max_iter=3000)
+        assert on["status"].tolist() == [0] * len(P) and on["iters"].tolist() == iters, (on["status"], on["iters"])
+        pr = ode_ref.Problem(ocp)
+        for b in range(len(P)):
+            kkt, gres = pr.kkt_residual(on["w"][b], on["lam_g"][b], on["lam_x"][b], P[b])
+            assert kkt <= 1e-6 and gres <= 1e-8, (ocp.model, b, kkt, gres)
