@@ -145,3 +145,17 @@ def test_shift_matches_reference_receding_horizon():
     X2, U2 = nlp_ref.split_w(w0, N)
     assert np.array_equal(X2[:, :N], X[:, 1:]) and np.array_equal(X2[:, N], X[:, N])
     assert np.array_equal(U2[:, :N - 1], U[:, 1:]) and np.array_equal(U2[:, N - 1], U[:, N - 1])
+
+
+def test_filter_harness_builds_and_exports():
+    """tests/hip/libfilter_check.so (the filter's device harness, tests/test_gpu_filter.py) is
+    built from the product's kernels.h and exports its two entry points; capacity >= 256."""
+    import subprocess
+
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hip")
+    subprocess.run(["make", "-C", here], check=True, capture_output=True)
+    lib = ctypes.CDLL(os.path.join(here, "libfilter_check.so"))
+    assert hasattr(lib, "filter_check")
+    for G in (16, 32, 64, 128, 256):
+        assert lib.filter_check_capacity(G) >= 256
+    assert lib.filter_check_capacity(8) == -1
