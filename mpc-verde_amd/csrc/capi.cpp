@@ -43,6 +43,9 @@ struct mpcx_handle {
   // restoration workspace of the models with a restoration phase (grown on demand)
   size_t cap_ws = 0;
   double* d_ws = nullptr;
+  // decoupled-suffix value functions across launches (SolveArgs::pcache)
+  double* d_pcache = nullptr;
+  double pc_epoch = 0, pc_gen = 1;
 };
 
 namespace {
@@ -388,6 +391,7 @@ void mpcx_destroy(mpcx_handle* h) {
   free_workspace(h);
   dev_free(h->d_sweep);
   dev_free(h->d_ws);
+  dev_free(h->d_pcache);
   free_linear(h);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -437,6 +441,7 @@ int mpcx_set_linear_model(mpcx_handle* h, int32_t n_tab, const double* A, const 
   }
   h->lin_ntab = n_tab;
   h->lin_rows = tab_rows;
+  h->pc_gen += 1;  // cached suffix value functions belong to the old tables
   h->lin_dec = 0;
   for (int j = 0; j < n_tab && j < 64; ++j) {
     bool d = true;
@@ -458,6 +463,7 @@ int mpcx_set_linear_tab_dev(mpcx_handle* h, const int32_t* d_tab, int32_t tab_ro
   if (d_tab && tab_rows < 1) return fail(MPCX_EINVAL, "tab_rows must be >= 1");
   h->ext_tab = d_tab;
   h->ext_rows = d_tab ? tab_rows : 0;
+  h->pc_gen += 1;  // the schedule (hence the suffix) may have changed
   return 0;
 }
 
@@ -548,6 +554,17 @@ static int solve_launch(mpcx_handle* h, mpcx::SolveArgs& a, hipStream_t stream) 
     a.ws_stride = threads;
   } else {
     a.restoration = 0;
+  }
+  if (a.model == MPCX_MODEL_LINEAR && h->lin_dec != 0) {
+    // decoupled-suffix value functions of earlier launches (kernels.h "decoupled suffix")
+    if (!h->d_pcache) {
+      const size_t n = (size_t)(a.N + 2) * (a.nx * (a.nx + 1) / 2);
+      HIPCHK(hipMalloc(&h->d_pcache, n * sizeof(double)));
+      HIPCHK(hipMemset(h->d_pcache, 0, n * sizeof(double)));  // header epoch 0: nothing cached
+    }
+    a.pcache = h->d_pcache;
+    a.pc_epoch = (h->pc_epoch += 1);
+    a.pc_gen = h->pc_gen;
   }
   HIPCHK(mpcx::launch_solve(a, stream));
   // instances parked at a failed line search continue in the resume launch (restoration)

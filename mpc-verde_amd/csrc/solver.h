@@ -42,6 +42,12 @@ struct SolveArgs {
   int restoration;      // soft restoration + restoration phase on a failed line search (models with kResto)
   double* ws;           // restoration workspace: slot i of thread t at ws[i * ws_stride + t] (kResto models)
   long ws_stride;
+  // linear models with a decoupled suffix: P_k of the suffix stages as a launch of this handle
+  // computed them at fs = 1, delta = 0 ((N + 1) x NP doubles, then the header {launch epoch,
+  // table generation, kb}), or null; pc_epoch = this launch (> every earlier one), pc_gen = the
+  // tables' generation (bumped by every table or schedule change)
+  double* pcache;
+  double pc_epoch, pc_gen;
   StageParams sp;       // unicycle constants
   LinTables lin;        // linear model tables
   OdeParams op;         // nonlinear ODE models
