@@ -159,3 +159,38 @@ def test_filter_harness_builds_and_exports():
     for G in (16, 32, 64, 128, 256):
         assert lib.filter_check_capacity(G) >= 256
     assert lib.filter_check_capacity(8) == -1
+
+
+def test_bench_group_size_and_usable_cpus():
+    """bench.py's lane-group rule (used to find the solve kernel's PMC record for its roofline)
+    is csrc/solver.h solve_group_size, and its CPU count for the baseline is every CPU the
+    process may run on (affinity mask, capped by a cgroup quota), never OMP_NUM_THREADS."""
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    def cpp_rule(N, B, n_simd, policy):  # csrc/solver.h solve_group_size
+        G = 16 if N < 16 else 32 if N < 32 else 64 if N < 64 else 128 if N < 128 else 256
+        if policy == 0:
+            while G < 64 and B * G * 2 <= 64 * n_simd:
+                G *= 2
+        return G
+
+    for N in (1, 10, 15, 16, 20, 30, 31, 32, 50, 63, 64, 100, 127, 128, 255):
+        for B in (1, 64, 1024, 2048, 4096, 100000):
+            for pol in (0, 1):
+                assert bench.group_size(N, B, 1024, pol) == cpp_rule(N, B, 1024, pol)
+    assert bench.group_size(20, 1024, 1024) == 64 and bench.group_size(30, 4096, 1024) == 32
+    old = os.environ.get("OMP_NUM_THREADS")
+    os.environ["OMP_NUM_THREADS"] = "1"
+    try:
+        n = bench.usable_cpus()
+    finally:
+        if old is None:
+            del os.environ["OMP_NUM_THREADS"]
+        else:
+            os.environ["OMP_NUM_THREADS"] = old
+    assert 1 <= n <= len(os.sched_getaffinity(0)) <= (os.cpu_count() or 1)
