@@ -402,3 +402,34 @@ def test_pendulum_run_equals_lockstep_decoupled_suffix(mpcx, dec, monkeypatch):
     assert np.all(np.array(st_l) == 0)
     for n in ("P", "w", "w0", "lam", "lamx", "f"):
         np.testing.assert_array_equal(getattr(run, n).cpu().numpy(), getattr(lock, n).cpu().numpy(), err_msg=n)
+
+
+def test_pendulum_suffix_cache_follows_table_changes(mpcx):
+    """The decoupled suffix's P_k cached across launches (capi SolveArgs::pcache) belong to one
+    table generation: after mpcx_set_linear_model with other weights (q), and after a schedule
+    change that moves the free/blocked boundary (n_free), a handle that has cached the old
+    suffix gives the same bits as a fresh handle of the new problem."""
+    from mpcx import lti
+
+    N, B = 100, 64
+    rng = np.random.default_rng(7)
+    x = rng.uniform([-1, -.5, -.2, -.5], [1, .5, .2, .5], size=(B, 4))
+    lin1 = lti.inverted_pendulum_qp(N=N)
+    lin2 = lti.inverted_pendulum_qp(N=N, q=(1.5, 2.0))
+    lin3 = lti.inverted_pendulum_qp(N=N, n_free=8)
+    S = mpcx.nlpsol("pc", "mi355x", lin1, {"ipopt": {"max_iter": 200}})
+    P = lti.pendulum_params(lin1, x, 0.0)
+    for _ in range(2):  # fill, then use, the cache of lin1
+        r1 = S.solve_batch(P)
+    ref1 = mpcx.nlpsol("pc1", "mi355x", lin1, {"ipopt": {"max_iter": 200}}).solve_batch(P)
+    np.testing.assert_array_equal(r1["w"], ref1["w"])
+    for lin in (lin2, lin3):
+        S.set_linear_model(lin)
+        r = S.solve_batch(P)
+        r_again = S.solve_batch(P)
+        ref = mpcx.nlpsol("pcf", "mi355x", lin, {"ipopt": {"max_iter": 200}}).solve_batch(P)
+        assert np.all(ref["status"] == 0)
+        for got in (r, r_again):
+            np.testing.assert_array_equal(got["w"], ref["w"])
+            np.testing.assert_array_equal(got["iters"], ref["iters"])
+        assert np.max(np.abs(r["w"] - r1["w"])) > 1e-6  # the problems really differ
