@@ -1660,6 +1660,11 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 
     STAMP(7);
     // ------------------------------------------------------------ update iterate
+#ifdef MPCX_DEBUG_PRINT
+    if (inst == 0 && k == 0 && !done && !handled)
+      printf("STEP it=%d resto=0 alpha=%.17g alpha_d=%.17g ftype=%d mu=%.17g delta=%.3g thk=%.17g phk=%.17g\n", it, alpha,
+             az, (int)ftype, mu, delta, thk, phk);
+#endif
     if (!done && !handled) {
       if (!ftype) {  // augment the filter
         if (filt.add((1.0 - kGammaTheta) * thk, phk - kGammaPhi * thk, k, xw)) DIAG(14);

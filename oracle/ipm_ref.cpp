@@ -1401,6 +1401,8 @@ int solve_one(Inst<Dyn>& I, double* w, double* lam, const oracle_opts& op, int* 
       }
     }
     // ---- update
+    TRACE("STEP it=%d resto=%d alpha=%.17g alpha_d=%.17g ftype=%d mu=%.17g delta=%.3g thk=%.17g phk=%.17g\n", it,
+          (int)resto, alpha, alpha_d, (int)ftype, mu, delta, thk, phk);
     for (int i = 0; i < nw; ++i) w[i] += alpha * dw[i];
     for (int i = 0; i < ng; ++i) lam[i] += alpha * (lamNew[i] - lam[i]);
     for (int i = 0; i < nw; ++i) {
