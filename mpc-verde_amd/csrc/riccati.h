@@ -206,8 +206,8 @@ __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp,
   return ok;
 }
 
-// The DEC step split in two, same operations: dec_prefactor (off the chain: the factors, which
-// need no p) and dec_vector_step (on the chain: s, gx, gu and p_k); P_k is the stored one.
+// The DEC step split in two: dec_prefactor (off the chain: the factors, which need no p) and
+// dec_vector_step (on the chain: s and p_k); P_k is the stored one.
 template <int NX, int NU>
 __device__ __forceinline__ bool dec_prefactor(const double* Hd, Fac<NX, NU>& f) {
   constexpr int NZ = NX + NU;
@@ -239,10 +239,15 @@ __device__ __forceinline__ bool dec_prefactor(const double* Hd, Fac<NX, NU>& f) 
   }
 }
 
+// On a decoupled stage B = 0 and Hux' = 0 exactly, so gu = gp_u and p_k = gx = gp_x + A^T s
+// (s = P_{k+1} c + p_{k+1}, vpre = P_{k+1} c): the full step's extra terms, B^T s and
+// -(L^{-1} Hux')^T D^{-1} L^{-1} gu', are exact zeros (they could change only the sign of an
+// exact zero), so the chain carries s and gx alone.
 template <int NX, int NU, unsigned long long AMASK, unsigned long long BMASK>
 __device__ __forceinline__ void dec_vector_step(const double* gp, const double* A, const double* Bm, const double* vpre,
                                                 const double* p, double* pn, Fac<NX, NU>& f) {
-  double s[NX], gx[NX], gu[NU];
+  (void)Bm;
+  double s[NX];
 #pragma unroll
   for (int i = 0; i < NX; ++i) s[i] = vpre[i] + p[i];
 #pragma unroll
@@ -251,32 +256,10 @@ __device__ __forceinline__ void dec_vector_step(const double* gp, const double* 
 #pragma unroll
     for (int m = 0; m < NX; ++m)
       if (AMASK & (1ull << (m * NX + i))) acc = fma(A[m * NX + i], s[m], acc);
-    gx[i] = acc;
+    pn[i] = acc;
   }
-#pragma unroll
-  for (int l = 0; l < NU; ++l) {
-    double acc = gp[NX + l];
-#pragma unroll
-    for (int m = 0; m < NX; ++m)
-      if (BMASK & (1ull << (m * NU + l))) acc = fma(Bm[m * NU + l], s[m], acc);
-    gu[l] = acc;
-  }
-  if constexpr (NU == 1) {
-    f.g0 = gu[0];
-#pragma unroll
-    for (int i = 0; i < NX; ++i) {
-      const double ri = f.r0 * f.h0[i];
-      pn[i] = fma(-ri, f.g0, gx[i]);
-    }
-  } else {
-    f.g0 = gu[0];
-    f.g1 = fma(-f.t, gu[0], gu[1]);
-#pragma unroll
-    for (int i = 0; i < NX; ++i) {
-      const double r0i = f.r0 * f.h0[i], r1i = f.r1 * f.h1[i];
-      pn[i] = fma(-r1i, f.g1, fma(-r0i, f.g0, gx[i]));
-    }
-  }
+  f.g0 = gp[NX];
+  if constexpr (NU == 2) f.g1 = fma(-f.t, gp[NX], gp[NX + 1]);
 }
 
 // K = -Huu'^{-1} Hux', kf = -Huu'^{-1} gu' from the LDL^T data (off the critical path).
