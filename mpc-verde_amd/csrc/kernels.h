@@ -932,6 +932,30 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         seq = gmin<G>(good ? 1.0 : 0.0, xw) < 0.5;
         DIAG_IF(seq && !done, 8);
       }
+      // Stash: the iterate, its bound multipliers, bounds and lam are live across the sequential
+      // chain but unused in it; for the 6-state model they go to the LDS value cache (idle
+      // between evaluations) so the chain's operands keep registers instead of scratch
+      constexpr bool kStash = !Model::kParallelRiccati && NX >= 6 && Model::kTrigSlots >= 5 * NZ + NX;
+      auto stash = [&](bool back) __attribute__((always_inline)) {
+        if constexpr (kStash) {
+          double* t = tcache + threadIdx.x;
+          auto mv = [&](double& v, int o) __attribute__((always_inline)) {
+            if (back) v = t[o * kSBS];
+            else t[o * kSBS] = v;
+          };
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) {
+            mv(z[i], i);
+            mv(zL[i], NZ + i);
+            mv(zU[i], 2 * NZ + i);
+            mv(lb[i], 3 * NZ + i);
+            mv(ub[i], 4 * NZ + i);
+          }
+#pragma unroll
+          for (int i = 0; i < NX; ++i) mv(lam[i], 5 * NZ + i);
+        }
+      };
+      stash(false);
       if (__any(seq)) {  // sequential recursion (models without the scan, or its fallback)
         if (seq) {
           okl = true;
@@ -1023,6 +1047,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           }
         }
       }
+      stash(true);
 #pragma unroll
       for (int i = 0; i < NP; ++i) Pk[i] = P[i];
 #pragma unroll
