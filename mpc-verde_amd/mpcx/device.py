@@ -51,6 +51,9 @@ class DeviceLoop:
     warm_start_init_point (spec.warm_*); the first solve is always cold.
     ``step()`` enqueues one fused solve + plant/shift launch on ``stream`` and
     returns immediately (``solve()`` / ``shift()`` do the two halves separately).
+    A linear model embedded in a larger kernel instantiation (``lti.StatePad``) takes P0 in
+    its own layout; the device tensors hold the kernel's padded layout
+    (``solver._pad.w_idx`` / ``p_idx`` / ``g_idx`` select the model's entries).
     """
 
     def __init__(self, solver: Solver, P0, device="cuda", stream=None, cold_first=True, warm_duals=True):
@@ -61,8 +64,12 @@ class DeviceLoop:
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         P0 = np.ascontiguousarray(np.asarray(P0, np.float64))
-        if P0.ndim != 2 or P0.shape[1] != solver._h.n_p:
-            raise ValueError(f"P0: expected (B, {solver._h.n_p}), got {P0.shape}")
+        if P0.ndim != 2 or P0.shape[1] != solver.n_p:
+            raise ValueError(f"P0: expected (B, {solver.n_p}), got {P0.shape}")
+        pd = getattr(solver, "_pad", None)
+        if pd is not None:
+            P0 = pd.scatter(P0, pd.p_idx, pd.n_p_pad)
+        self._knx = pd.nxp if pd is not None else solver.ocp.nx  # states of the kernel layout
         self.B = P0.shape[0]
         nw, ng = solver._h.n_w, solver._h.n_g
         z = lambda *s: torch.zeros(s, dtype=torch.float64, device=self.device)  # noqa: E731
@@ -105,7 +112,7 @@ class DeviceLoop:
         """Per-step stage references (tracking, param layout x0_stageref): refs is a
         (B, N*(nx+nu)) float64 device tensor copied into P[:, nx:] on the loop's stream
         (Trajectory_tracking.py:105-106 sets solver.par["p", k] each step)."""
-        nx = self.solver.ocp.nx
+        nx = self._knx
         _check(refs, "refs", torch.float64, (self.B, self.P.shape[1] - nx), self.device)
         with torch.cuda.stream(self.stream):
             self.P[:, nx:].copy_(refs, non_blocking=True)

@@ -139,6 +139,79 @@ class LinearOCP:
         return np.ascontiguousarray(np.concatenate([x0, zr.reshape(Bn, -1)], axis=1))
 
 
+# (nx, nu) shapes with a kernel instantiation (csrc/solve_linear4.hip, solve_linear5.hip)
+NATIVE_SHAPES = ((4, 1), (5, 1))
+
+
+class StatePad:
+    """A linear OCP with fewer states than a kernel instantiation, embedded in it.
+
+    nx < 4, nu = 1 is solved as the 4-state model with zero pad states: A, B, c and W are
+    zero-padded (pad rows and columns of A and W are 0, pad rows of B and c are 0) and the
+    pad states are unbounded.  A pad state then starts at 0 (x0 and references padded with
+    0), its defect is 0 at every iterate and so is every Newton step in it (its row of the
+    dynamics maps everything to 0), its Riccati blocks are 0 and the inertia test sees the
+    same Huu' as the unpadded problem: the solve is the same QP, with the same optimum and
+    multipliers.  One IPOPT quantity sees the pad: the dual scaling s_d averages the
+    multipliers over n_g + n_w entries, which include the pad's zero entries -- it differs from
+    1 only when that mean exceeds s_max = 100 (Wächter & Biegler 2006 eq. 5).
+    The index maps take the user's (B, n) arrays to the kernel's layout and back: w = [X_0 |
+    U_k X_{k+1}]_k, P = [x0 | (x_r, u_r)_k], g = [g_k (nx)]_k.
+    """
+
+    def __init__(self, lin: LinearOCP, nxp: int = 4):
+        nx, nu, N = lin.nx, lin.nu, lin.N
+        if nx >= nxp:
+            raise ValueError(f"StatePad: nx = {nx} needs no padding to {nxp}")
+        self.lin, self.nxp = lin, nxp
+        nzp = nxp + nu
+        ix = np.r_[np.arange(nx), nxp + np.arange(nu)]  # z = (x, u) -> padded z = (x, pad, u)
+        A = np.zeros((lin.n_tab, nxp, nxp))
+        A[:, :nx, :nx] = lin.A
+        Bm = np.zeros((lin.n_tab, nxp, nu))
+        Bm[:, :nx] = lin.B
+        c = np.zeros((lin.n_tab, nxp))
+        c[:, :nx] = lin.c
+        W = np.zeros((lin.n_tab, nzp, nzp))
+        W[:, ix[:, None], ix[None, :]] = lin.W
+        pad = (nxp - nx,)
+        self.ocp = dataclasses.replace(lin, A=A, B=Bm, c=c, W=W, tab=lin.tab.copy(),
+                                       x_lb=tuple(lin.x_lb) + (-math.inf,) * pad[0],
+                                       x_ub=tuple(lin.x_ub) + (math.inf,) * pad[0])
+        self.w_idx = np.concatenate([np.arange(nx)] + [nxp + nzp * k + np.r_[np.arange(nu), nu + np.arange(nx)]
+                                                       for k in range(N)])
+        self.p_idx = np.concatenate([np.arange(nx)] + [nxp + nzp * k + ix for k in range(N)])
+        self.g_idx = np.concatenate([nxp * k + np.arange(nx) for k in range(N + 1)])
+        self.n_w, self.n_p, self.n_g = self.w_idx.size, self.p_idx.size, self.g_idx.size
+        self.n_w_pad, self.n_p_pad, self.n_g_pad = self.ocp.n_w_ms, self.ocp.n_p, self.ocp.n_g_ms
+
+    @staticmethod
+    def scatter(a, idx, n, fill=0.0):
+        """(B, len(idx)) user array -> (B, n) kernel array, `fill` in the pad entries."""
+        if a is None:
+            return None
+        a = np.atleast_2d(np.asarray(a, np.float64))
+        out = np.full((a.shape[0], n), fill)
+        out[:, idx] = a
+        return np.ascontiguousarray(out)
+
+    @staticmethod
+    def gather(a, idx):
+        """(B, n) kernel array -> (B, len(idx)) user array."""
+        return None if a is None else np.ascontiguousarray(a[:, idx])
+
+
+def state_pad(lin) -> StatePad | None:
+    """The embedding a LinearOCP needs to run on a kernel instantiation, or None (native shape).
+    Raises for shapes no instantiation covers (nu != 1 or nx > 5)."""
+    if getattr(lin, "model", None) != "linear" or (lin.nx, lin.nu) in NATIVE_SHAPES:
+        return None
+    if lin.nu == 1 and lin.nx < 4:
+        return StatePad(lin, 4)
+    raise ValueError(f"linear model ({lin.nx} states, {lin.nu} inputs): the kernel is instantiated for "
+                     f"{NATIVE_SHAPES}; nx < 4 with one input is embedded in the 4-state model")
+
+
 # ----------------------------------------------------------------------------
 # Cart-pole set-point QP (config 5 family)
 # ----------------------------------------------------------------------------

@@ -27,7 +27,7 @@ import time
 import numpy as np
 
 from . import _lib
-from .lti import LinearOCP
+from .lti import LinearOCP, state_pad
 from .ocp import IPOPT_OPTIONS, OCP, to_spec
 from .ode import OdeOCP
 
@@ -49,6 +49,8 @@ def _vec(v, n, name, fill=None):
 class Solver:
     """Callable returned by :func:`nlpsol`."""
 
+    _pad = None  # lti.StatePad of a linear model embedded in a larger kernel instantiation
+
     def __init__(self, name: str, ocp: OCP, opts: dict | None = None, device: int = 0):
         opts = dict(opts or {})
         ip = dict(opts.get("ipopt", {}))
@@ -68,10 +70,13 @@ class Solver:
         # results); restoration (False: a failed line search ends the solve, IPOPT has no such switch)
         self.group_policy = int(opts.get("group_policy", 0))
         self.restoration = bool(opts.get("restoration", True))
-        self._h = _lib.Handle(to_spec(ocp, self.max_iter, self.tol, device, group_policy=self.group_policy, ipopt=term,
+        # a linear model without its own kernel instantiation runs embedded in one (lti.StatePad)
+        self._pad = state_pad(ocp)
+        kocp = self._pad.ocp if self._pad else ocp
+        self._h = _lib.Handle(to_spec(kocp, self.max_iter, self.tol, device, group_policy=self.group_policy, ipopt=term,
                                       restoration=self.restoration))
         if ocp.model == "linear":
-            self._h.set_linear_model(ocp)
+            self._h.set_linear_model(kocp)
         self._stats = {}
 
     def set_linear_model(self, lin=None):
@@ -80,16 +85,27 @@ class Solver:
             if lin.model != "linear" or (lin.nx, lin.nu, lin.N) != (self.ocp.nx, self.ocp.nu, self.ocp.N):
                 raise ValueError("set_linear_model: incompatible problem")
             self.ocp = lin
-        self._h.set_linear_model(self.ocp)
+        if self._pad is not None:
+            self._pad = state_pad(self.ocp)
+        self._h.set_linear_model(self._pad.ocp if self._pad else self.ocp)
 
     # ---------------------------------------------------------------- layout
     @property
     def n_w(self):
-        return self.ocp.N * self.ocp.nu if self.ocp.formulation == "single_shooting" else self._h.n_w
+        return self.ocp.N * self.ocp.nu if self.ocp.formulation == "single_shooting" else self._ms_nw
 
     @property
     def n_g(self):
-        return self.ocp.N * self._ss_ng if self.ocp.formulation == "single_shooting" else self._h.n_g
+        return self.ocp.N * self._ss_ng if self.ocp.formulation == "single_shooting" else self._ms_ng
+
+    @property
+    def _ms_nw(self):
+        """Multiple-shooting layout sizes of the user's problem (the kernel's unless padded)."""
+        return self._pad.n_w if self._pad else self._h.n_w
+
+    @property
+    def _ms_ng(self):
+        return self._pad.n_g if self._pad else self._h.n_g
 
     @property
     def _ss_ng(self):
@@ -99,7 +115,7 @@ class Solver:
 
     @property
     def n_p(self):
-        return self._h.n_p
+        return self._pad.n_p if self._pad else self._h.n_p
 
     def stats(self):
         return dict(self._stats)
@@ -116,9 +132,9 @@ class Solver:
         """
         P = np.ascontiguousarray(np.atleast_2d(np.asarray(P, np.float64)))
         B = P.shape[0]
-        if P.shape[1] != self._h.n_p:
-            raise ValueError(f"P: expected {self._h.n_p} columns, got {P.shape[1]}")
-        nw, ng = self._h.n_w, self._h.n_g
+        if P.shape[1] != self.n_p:
+            raise ValueError(f"P: expected {self.n_p} columns, got {P.shape[1]}")
+        nw, ng = self._ms_nw, self._ms_ng
         w0a = None
         if w0 is not None:
             w0a = np.ascontiguousarray(np.asarray(w0, np.float64).reshape(B, nw))
@@ -126,6 +142,15 @@ class Solver:
         ubw = _vec(ubw, nw, "ubw")
         l0 = None if lam_g0 is None else np.ascontiguousarray(np.asarray(lam_g0, np.float64).reshape(B, ng))
         lx0 = None if lam_x0 is None else np.ascontiguousarray(np.asarray(lam_x0, np.float64).reshape(B, nw))
+        pd = self._pad
+        if pd is not None:  # user layout -> the kernel's padded layout (pad states unbounded, 0)
+            P = pd.scatter(P, pd.p_idx, pd.n_p_pad)
+            w0a = pd.scatter(w0a, pd.w_idx, pd.n_w_pad)
+            lbw = None if lbw is None else pd.scatter(lbw[None, :], pd.w_idx, pd.n_w_pad, -1e20)[0]
+            ubw = None if ubw is None else pd.scatter(ubw[None, :], pd.w_idx, pd.n_w_pad, 1e20)[0]
+            l0 = pd.scatter(l0, pd.g_idx, pd.n_g_pad)
+            lx0 = pd.scatter(lx0, pd.w_idx, pd.n_w_pad)
+            nw, ng = pd.n_w_pad, pd.n_g_pad
         w = np.empty((B, nw))
         f = np.empty(B)
         lam = np.empty((B, ng)) if want_lam else None
@@ -139,6 +164,9 @@ class Solver:
                                         _lib.dptr(lbw), _lib.dptr(ubw), _lib.dptr(w), _lib.dptr(f), _lib.dptr(g),
                                         _lib.dptr(lam), _lib.dptr(lamx), _lib.iptr(st), _lib.iptr(it)))
         t = time.perf_counter() - t0
+        if pd is not None:
+            w, lamx = pd.gather(w, pd.w_idx), pd.gather(lamx, pd.w_idx)
+            lam, g = pd.gather(lam, pd.g_idx), pd.gather(g, pd.g_idx)
         return {"w": w, "f": f, "lam_g": lam, "lam_x": lamx, "g": g, "status": st, "iters": it, "t_wall": t}
 
     def rk4_sens(self, w, P):
@@ -180,7 +208,7 @@ class Solver:
         if p is None:
             raise ValueError("p is required")
         ocp = self.ocp
-        P = _vec(p, self._h.n_p, "p")[None, :]
+        P = _vec(p, self.n_p, "p")[None, :]
         ss = ocp.formulation == "single_shooting"
         lbx = _vec(lbx, self.n_w, "lbx", -math.inf)
         ubx = _vec(ubx, self.n_w, "ubx", math.inf)
@@ -209,9 +237,9 @@ class Solver:
                 w0 = np.concatenate([X[0]] + [np.concatenate([U[k], X[k + 1]]) for k in range(N)])[None, :]
         else:
             lbw, ubw = lbx, ubx
-            w0 = None if x0 is None else _vec(x0, self._h.n_w, "x0")[None, :]
-            l0 = None if lam_g0 is None else _vec(lam_g0, self._h.n_g, "lam_g0")[None, :]
-            lx0 = None if lam_x0 is None else _vec(lam_x0, self._h.n_w, "lam_x0")[None, :]
+            w0 = None if x0 is None else _vec(x0, self.n_w, "x0")[None, :]
+            l0 = None if lam_g0 is None else _vec(lam_g0, self.n_g, "lam_g0")[None, :]
+            lx0 = None if lam_x0 is None else _vec(lam_x0, self.n_w, "lam_x0")[None, :]
         lbw = np.where(np.isfinite(lbw), lbw, -1e20)
         ubw = np.where(np.isfinite(ubw), ubw, 1e20)
         r = self.solve_batch(P, w0, np.ascontiguousarray(lbw), np.ascontiguousarray(ubw), want_lam=True,
@@ -227,9 +255,9 @@ class Solver:
             g = Xs[:, 0:self._ss_ng].reshape(-1)
             lx = np.concatenate([lam_x[nx + nz * k:nx + nz * k + nu] for k in range(N)])
             return {"x": U[:, None], "f": np.array([[r["f"][0]]]), "g": g[:, None],
-                    "lam_g": np.zeros((self.n_g, 1)), "lam_x": lx[:, None], "lam_p": np.zeros((self._h.n_p, 1))}
+                    "lam_g": np.zeros((self.n_g, 1)), "lam_x": lx[:, None], "lam_p": np.zeros((self.n_p, 1))}
         return {"x": w[:, None], "f": np.array([[r["f"][0]]]), "g": r["g"][0][:, None],
-                "lam_g": r["lam_g"][0][:, None], "lam_x": lam_x[:, None], "lam_p": np.zeros((self._h.n_p, 1))}
+                "lam_g": r["lam_g"][0][:, None], "lam_x": lam_x[:, None], "lam_p": np.zeros((self.n_p, 1))}
 
     def _rollout(self, P, U):
         """X_{k+1} = F(X_k, U_k) on the plant kernel, stage k's references in the stage-0 slot."""
@@ -257,33 +285,42 @@ class Integrator:
 
     def __init__(self, ocp: OCP, device: int = 0, handle=None):
         self.ocp = ocp
-        self._h = handle if handle is not None else _lib.Handle(to_spec(ocp, device=device))
+        self._pad = state_pad(ocp)
+        kocp = self._pad.ocp if self._pad else ocp
+        self._h = handle if handle is not None else _lib.Handle(to_spec(kocp, device=device))
         if handle is None and ocp.model == "linear":
-            self._h.set_linear_model(ocp)
+            self._h.set_linear_model(kocp)
+
+    @property
+    def n_p(self):
+        return self._pad.n_p if self._pad else self._h.n_p
 
     def batch(self, P, U):
         P = np.ascontiguousarray(np.atleast_2d(np.asarray(P, np.float64)))
         U = np.ascontiguousarray(np.atleast_2d(np.asarray(U, np.float64)))
         B = P.shape[0]
         nx, nu = self.ocp.nx, self.ocp.nu
-        if P.shape[1] != self._h.n_p:
-            raise ValueError(f"P must be (B, {self._h.n_p})")
+        if P.shape[1] != self.n_p:
+            raise ValueError(f"P must be (B, {self.n_p})")
         if U.shape != (B, nu):
             raise ValueError(f"U must be (B, {nu})")
-        xf = np.empty((B, nx))
+        pd = self._pad
+        if pd is not None:
+            P = pd.scatter(P, pd.p_idx, pd.n_p_pad)
+        xf = np.empty((B, pd.nxp if pd else nx))
         qf = np.empty(B)
         _lib.check(_lib.load().mpcx_plant_step(self._h.ptr, B, _lib.dptr(P), _lib.dptr(U), _lib.dptr(xf),
                                                _lib.dptr(qf)))
-        return xf, qf
+        return np.ascontiguousarray(xf[:, :nx]), qf
 
     def __call__(self, *args, **kw):
         if kw:
             p = kw.get("x0")
             u = kw.get("p")
-            xf, qf = self.batch(_vec(p, self._h.n_p, "x0")[None, :], _vec(u, self.ocp.nu, "p")[None, :])
+            xf, qf = self.batch(_vec(p, self.n_p, "x0")[None, :], _vec(u, self.ocp.nu, "p")[None, :])
             return {"xf": xf[0][:, None], "qf": qf[:, None]}
         p, u = args
-        xf, qf = self.batch(_vec(p, self._h.n_p, "p")[None, :], _vec(u, self.ocp.nu, "u")[None, :])
+        xf, qf = self.batch(_vec(p, self.n_p, "p")[None, :], _vec(u, self.ocp.nu, "u")[None, :])
         return [xf[0][:, None], qf[:, None]]
 
 

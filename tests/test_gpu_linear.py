@@ -295,12 +295,12 @@ def test_ltv_device_loop_with_device_schedule(mpcx, R):
     loop.set_schedule(None)
 
 
-@pytest.mark.parametrize("nx,seed", [(4, 0), (4, 1), (5, 2), (5, 3)])
+@pytest.mark.parametrize("nx,seed", [(4, 0), (4, 1), (5, 2), (5, 3), (1, 4), (2, 5), (3, 6)])
 def test_random_linear_problems_vs_lq_oracle(mpcx, R, nx, seed):
     """Random LTV problems through the generic linear path: 3 tables of random stable A
     (spectral radius 0.95), random B, c, SPD stage weights, per-instance random schedules,
     random per-stage references, |u| <= 1 so that bounds are active; N = 1, 12, 40 and 100
-    (nx = 4 runs the log-depth Riccati scan with table operands: single-wave groups, and at
+    (nx < 4 runs embedded in the 4-state model, lti.StatePad; nx = 4 runs the log-depth Riccati scan with table operands: single-wave groups, and at
     N = 100 a two-wave group whose scan crosses waves through LDS).
     Random problems include degenerate bounds (multiplier ~ 0 at an active bound), where an
     interior-point solution at tol 1e-8 is O(sqrt(mu)) from the vertex -- as IPOPT's would be:
@@ -433,3 +433,83 @@ def test_pendulum_suffix_cache_follows_table_changes(mpcx):
             np.testing.assert_array_equal(got["w"], ref["w"])
             np.testing.assert_array_equal(got["iters"], ref["iters"])
         assert np.max(np.abs(r["w"] - r1["w"])) > 1e-6  # the problems really differ
+
+
+def test_padded_double_integrator_closed_loop(mpcx, R):
+    """A 2-state model (double integrator, no kernel instantiation of its own) through the
+    CasADi-shaped call and the integrator, in the reference's closed-loop pattern
+    (solve, apply u_0 through F, shift): every step's inputs match the LQ oracle, F matches
+    A x + B u + c, and the returned multipliers / g have the user's (unpadded) sizes."""
+    from mpcx import lti
+
+    T, N = 0.1, 20
+    A = np.array([[1.0, T], [0.0, 1.0]])
+    Bm = np.array([[0.5 * T * T], [T]])
+    W = np.diag([1.0, 0.1, 0.01])
+    lin = lti.LinearOCP(N=N, A=A[None], B=Bm[None], W=W[None], tab=np.zeros(N, np.int32), u_lb=(-1.0,), u_ub=(1.0,))
+    S = mpcx.nlpsol("dint", "mi355x", lin, {"ipopt": {"max_iter": 200}})
+    F = mpcx.integrator(lin)
+    assert (S.n_w, S.n_g, S.n_p) == (2 + 3 * N, 2 * (N + 1), 2 + 3 * N)
+    x = np.array([5.0, 0.0])
+    zr = np.zeros((N, 3))
+    lbx = np.full(S.n_w, -np.inf)
+    ubx = np.full(S.n_w, np.inf)
+    lbx[2::3], ubx[2::3] = -1.0, 1.0  # CasADi-style: the input bounds come with the call
+    w0 = None
+    for t in range(60):
+        p = lin.params(x, zr)[0]
+        sol = S(x0=w0, p=p, lbx=lbx, ubx=ubx)
+        assert S.stats()["success"], t
+        assert sol["x"].shape == (S.n_w, 1) and sol["lam_g"].shape == (S.n_g, 1) and sol["g"].shape == (S.n_g, 1)
+        w = sol["x"][:, 0]
+        _, U_ref, _ = R.lq_solve(x, lin.A, lin.B, lin.c, lin.W, lin.tab, zr, [-1.0], [1.0])
+        # bang-bang inputs leave the bound with a multiplier ~ 0 (degenerate): an interior point
+        # at tol 1e-8 is O(sqrt(mu)) from the vertex there, as in the random problems above
+        assert rel(w[2::3], U_ref[:, 0]) <= 1e-4, t
+        assert np.max(np.abs(sol["g"])) <= 1e-8
+        xf = F(p, w[2])[0][:, 0]
+        np.testing.assert_allclose(xf, A @ x + Bm[:, 0] * w[2], rtol=1e-14, atol=1e-14)
+        x = xf
+        w0 = np.concatenate([w[0:2] * 0 + x, w[5:], w[-3:]])  # shifted guess (X_0 = new state)
+    assert abs(x[0]) < 1.0  # driven towards the origin under |u| <= 1
+
+
+def test_padded_model_device_loop(mpcx, R):
+    """DeviceLoop on a 3-state model embedded in the 4-state kernel: P0 in the model's layout,
+    device state in the kernel's (pad states 0 throughout), u_0 of every warm-started step
+    equal to the LQ oracle's, the plant-updated state equal to A x + B u + c."""
+    import torch
+    from mpcx import lti
+    from mpcx.device import DeviceLoop
+
+    rng = np.random.default_rng(21)
+    nx, N, B = 3, 15, 16
+    A = rng.normal(size=(nx, nx))
+    A = 0.98 * A / max(abs(np.linalg.eigvals(A)))
+    Bm = rng.normal(size=(nx, 1))
+    c = 0.05 * rng.normal(size=nx)
+    M = rng.normal(size=(nx + 1, nx + 1))
+    W = M @ M.T / 4 + 0.1 * np.eye(nx + 1)
+    lin = lti.LinearOCP(N=N, A=A[None], B=Bm[None], c=c[None], W=W[None], tab=np.zeros(N, np.int32),
+                        u_lb=(-0.5,), u_ub=(0.5,))
+    S = mpcx.nlpsol("pad3", "mi355x", lin, {"ipopt": {"max_iter": 200}})
+    pd = S._pad
+    assert pd is not None and pd.nxp == 4
+    x = 2.0 * rng.normal(size=(B, nx))
+    zr = np.zeros((N, nx + 1))
+    loop = DeviceLoop(S, lin.params(x, zr), device="cuda:0")
+    for step in range(8):
+        loop.step()
+        torch.cuda.synchronize()
+        assert np.all(loop.status.cpu().numpy() == 0), step
+        wk = loop.w.cpu().numpy()
+        assert np.all(wk.reshape(B, -1)[:, 3:4] == 0)  # X_0's pad entry
+        w = pd.gather(wk, pd.w_idx)
+        for b in range(B):
+            _, U_ref, _ = R.lq_solve(x[b], lin.A, lin.B, lin.c, lin.W, lin.tab, zr, [-0.5], [0.5])
+            # random bounded problem: near-degenerate bounds, held to the north-star 1e-4 (see above)
+            assert rel(w[b, nx::nx + 1], U_ref[:, 0]) <= 1e-4, (step, b)
+        x = x @ A.T + w[:, nx:nx + 1] * Bm[:, 0][None, :] + c
+        Pk = loop.P.cpu().numpy()
+        np.testing.assert_allclose(Pk[:, 0:nx], x, rtol=1e-12, atol=1e-12)
+        assert np.all(Pk[:, nx:4] == 0)
