@@ -45,7 +45,8 @@ enum mpcx_model {
   /* x+ = A_j x + B_j u + c_j, l = (z - zr_k)^T W_j (z - zr_k), z = (x, u): the mpctools
      LTI/LTV QPs (Inverted_pendulum/inverted_pendulum_single_shooting_mpctools.py:19-64,
      Trajectory Tracking/Trajectory_tracking_dynamic_model.py:117-145); tables set with
-     mpcx_set_linear_model.  (nx, nu) in {(4,1), (5,1)}. */
+     mpcx_set_linear_model.  (nx, nu) in {(4,1), (5,1), (4,2)}; smaller models
+     embed with zero pad states (mpcx/lti.py StatePad). */
   MPCX_MODEL_LINEAR = 2,
   /* Nonlinear ODE models (BASELINE config variants; parity against the CPU oracle only),
      RK4 with M substeps, node cost l = sum Q_i (x_i - xr_i)^2 + sum R_j (u_j - ur_j)^2,

@@ -321,8 +321,9 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
   if (s->model != MPCX_MODEL_UNICYCLE && s->model != MPCX_MODEL_LINEAR && !is_ode(s->model))
     return fail(MPCX_EINVAL, "unknown model");
   if (is_ode(s->model) && s->cost != MPCX_COST_NODE) return fail(MPCX_EINVAL, "ODE models use MPCX_COST_NODE");
-  if (s->model == MPCX_MODEL_LINEAR && !((s->nx == 4 && s->nu == 1) || (s->nx == 5 && s->nu == 1)))
-    return fail(MPCX_EINVAL, "linear model: (nx, nu) must be (4, 1) or (5, 1)");
+  if (s->model == MPCX_MODEL_LINEAR &&
+      !((s->nx == 4 && s->nu == 1) || (s->nx == 5 && s->nu == 1) || (s->nx == 4 && s->nu == 2)))
+    return fail(MPCX_EINVAL, "linear model: (nx, nu) must be (4, 1), (5, 1) or (4, 2)");
   if (s->N < 1 || s->N > 255) return fail(MPCX_EINVAL, "N must be in [1, 255]");
   if (s->M < 1 || s->M > 64) return fail(MPCX_EINVAL, "M must be in [1, 64]");
   if ((s->model == MPCX_MODEL_UNICYCLE || is_ode(s->model)) && !(s->T > 0)) return fail(MPCX_EINVAL, "T must be > 0");

@@ -107,6 +107,7 @@ MPCX_DECLARE(unicycle)
 MPCX_DECLARE(unicycle_scan)
 MPCX_DECLARE(linear4)
 MPCX_DECLARE(linear5)
+MPCX_DECLARE(linear4x2)
 MPCX_DECLARE(kin_bicycle)
 MPCX_DECLARE(dyn_bicycle)
 MPCX_DECLARE(cartpole)
@@ -116,13 +117,14 @@ MPCX_DECLARE(cartpole)
 constexpr int kUnicycleScanMinN = 25;
 
 // unicycle, the linear-model shapes the reference's QPs need (4x1 lateral / cart-pole, 5x1
-// cart-pole with the previous input as a state), and the BASELINE's nonlinear ODE variants
+// cart-pole with the previous input as a state; 4x2 for two-input models), and the BASELINE's nonlinear ODE variants
 #define MPCX_DISPATCH(a, FN, ...)                                                 \
   do {                                                                            \
     if ((a).model == 1)                                                           \
       return (a).N >= kUnicycleScanMinN ? FN##_unicycle_scan(__VA_ARGS__) : FN##_unicycle(__VA_ARGS__); \
     if ((a).model == 2 && (a).nx == 4 && (a).nu == 1) return FN##_linear4(__VA_ARGS__); \
     if ((a).model == 2 && (a).nx == 5 && (a).nu == 1) return FN##_linear5(__VA_ARGS__); \
+    if ((a).model == 2 && (a).nx == 4 && (a).nu == 2) return FN##_linear4x2(__VA_ARGS__); \
     if ((a).model == 3) return FN##_kin_bicycle(__VA_ARGS__);                     \
     if ((a).model == 4) return FN##_dyn_bicycle(__VA_ARGS__);                     \
     if ((a).model == 5) return FN##_cartpole(__VA_ARGS__);                        \
@@ -148,12 +150,12 @@ hipError_t launch_shift(const SolveArgs& a, double* P, const double* W, double* 
 // diagnostic build: every model unit holds its own copy of the buffer pointers
 extern "C" int mpcx_diag_set_stamp_buffer(void* d_buf) {
   using namespace mpcx;
-  return diag_set_stamps_unicycle(d_buf) | diag_set_stamps_unicycle_scan(d_buf) | diag_set_stamps_linear4(d_buf) | diag_set_stamps_linear5(d_buf) |
+  return diag_set_stamps_unicycle(d_buf) | diag_set_stamps_unicycle_scan(d_buf) | diag_set_stamps_linear4(d_buf) | diag_set_stamps_linear5(d_buf) | diag_set_stamps_linear4x2(d_buf) |
          diag_set_stamps_kin_bicycle(d_buf) | diag_set_stamps_dyn_bicycle(d_buf) | diag_set_stamps_cartpole(d_buf);
 }
 extern "C" int mpcx_diag_set_counter_buffer(void* d_buf) {
   using namespace mpcx;
-  return diag_set_counters_unicycle(d_buf) | diag_set_counters_unicycle_scan(d_buf) | diag_set_counters_linear4(d_buf) | diag_set_counters_linear5(d_buf) |
+  return diag_set_counters_unicycle(d_buf) | diag_set_counters_unicycle_scan(d_buf) | diag_set_counters_linear4(d_buf) | diag_set_counters_linear5(d_buf) | diag_set_counters_linear4x2(d_buf) |
          diag_set_counters_kin_bicycle(d_buf) | diag_set_counters_dyn_bicycle(d_buf) | diag_set_counters_cartpole(d_buf);
 }
 #endif

@@ -139,14 +139,15 @@ class LinearOCP:
         return np.ascontiguousarray(np.concatenate([x0, zr.reshape(Bn, -1)], axis=1))
 
 
-# (nx, nu) shapes with a kernel instantiation (csrc/solve_linear4.hip, solve_linear5.hip)
-NATIVE_SHAPES = ((4, 1), (5, 1))
+# (nx, nu) shapes with a kernel instantiation (csrc/solve_linear4.hip, solve_linear5.hip,
+# solve_linear4x2.hip)
+NATIVE_SHAPES = ((4, 1), (5, 1), (4, 2))
 
 
 class StatePad:
     """A linear OCP with fewer states than a kernel instantiation, embedded in it.
 
-    nx < 4, nu = 1 is solved as the 4-state model with zero pad states: A, B, c and W are
+    nx < 4 with nu = 1 or 2 is solved as the 4-state model of the same nu with zero pad states: A, B, c and W are
     zero-padded (pad rows and columns of A and W are 0, pad rows of B and c are 0) and the
     pad states are unbounded.  A pad state then starts at 0 (x0 and references padded with
     0), its defect is 0 at every iterate and so is every Newton step in it (its row of the
@@ -203,13 +204,13 @@ class StatePad:
 
 def state_pad(lin) -> StatePad | None:
     """The embedding a LinearOCP needs to run on a kernel instantiation, or None (native shape).
-    Raises for shapes no instantiation covers (nu != 1 or nx > 5)."""
+    Raises for shapes no instantiation covers (nu > 2, or nx > 4 unless (5, 1))."""
     if getattr(lin, "model", None) != "linear" or (lin.nx, lin.nu) in NATIVE_SHAPES:
         return None
-    if lin.nu == 1 and lin.nx < 4:
+    if lin.nu in (1, 2) and lin.nx < 4:
         return StatePad(lin, 4)
     raise ValueError(f"linear model ({lin.nx} states, {lin.nu} inputs): the kernel is instantiated for "
-                     f"{NATIVE_SHAPES}; nx < 4 with one input is embedded in the 4-state model")
+                     f"{NATIVE_SHAPES}; nx < 4 with one or two inputs is embedded in the 4-state model")
 
 
 # ----------------------------------------------------------------------------

@@ -295,12 +295,14 @@ def test_ltv_device_loop_with_device_schedule(mpcx, R):
     loop.set_schedule(None)
 
 
-@pytest.mark.parametrize("nx,seed", [(4, 0), (4, 1), (5, 2), (5, 3), (1, 4), (2, 5), (3, 6)])
-def test_random_linear_problems_vs_lq_oracle(mpcx, R, nx, seed):
+@pytest.mark.parametrize("nx,nu,seed", [(4, 1, 0), (4, 1, 1), (5, 1, 2), (5, 1, 3), (1, 1, 4), (2, 1, 5), (3, 1, 6),
+                                        (4, 2, 7), (3, 2, 8), (2, 2, 9)])
+def test_random_linear_problems_vs_lq_oracle(mpcx, R, nx, nu, seed):
     """Random LTV problems through the generic linear path: 3 tables of random stable A
     (spectral radius 0.95), random B, c, SPD stage weights, per-instance random schedules,
     random per-stage references, |u| <= 1 so that bounds are active; N = 1, 12, 40 and 100
-    (nx < 4 runs embedded in the 4-state model, lti.StatePad; nx = 4 runs the log-depth Riccati scan with table operands: single-wave groups, and at
+    (nu = 2: the LinearModel<4, 2> instantiation; nx < 4 runs embedded in the 4-state model of
+    the same nu, lti.StatePad; nx = 4 runs the log-depth Riccati scan with table operands: single-wave groups, and at
     N = 100 a two-wave group whose scan crosses waves through LDS).
     Random problems include degenerate bounds (multiplier ~ 0 at an active bound), where an
     interior-point solution at tol 1e-8 is O(sqrt(mu)) from the vertex -- as IPOPT's would be:
@@ -309,7 +311,7 @@ def test_random_linear_problems_vs_lq_oracle(mpcx, R, nx, seed):
     from mpcx import lti
 
     rng = np.random.default_rng(seed)
-    nu, n_tab, B = 1, 3, 48
+    n_tab, B = 3, 48
     nz = nx + nu
     As, Bs, cs, Ws = [], [], [], []
     for _ in range(n_tab):
@@ -322,17 +324,17 @@ def test_random_linear_problems_vs_lq_oracle(mpcx, R, nx, seed):
     for N in (1, 12, 40, 100):
         tab = rng.integers(0, n_tab, size=(B, N)).astype(np.int32)
         lin = lti.LinearOCP(N=N, A=np.stack(As), B=np.stack(Bs), c=np.stack(cs), W=np.stack(Ws), tab=tab,
-                            u_lb=(-1.0,), u_ub=(1.0,))
+                            u_lb=(-1.0,) * nu, u_ub=(1.0,) * nu)
         S = mpcx.nlpsol("rnd", "mi355x", lin, {"ipopt": {"max_iter": 500}})
         x0 = 3.0 * rng.normal(size=(B, nx))
         zr = rng.normal(size=(B, N, nz))
         r = S.solve_batch(lin.params(x0, zr))
         assert np.all(r["status"] == 0), np.unique(r["status"], return_counts=True)
-        U = U_of(r["w"], nx, nu, N)[..., 0]
+        U = U_of(r["w"], nx, nu, N)
         n_active = 0
         for b in range(B):
-            _, U_ref, J = R.lq_solve(x0[b], lin.A, lin.B, lin.c, lin.W, tab[b], zr[b], [-1.0], [1.0])
-            assert rel(U[b], U_ref[:, 0]) <= 1e-4, (N, b)
+            _, U_ref, J = R.lq_solve(x0[b], lin.A, lin.B, lin.c, lin.W, tab[b], zr[b], [-1.0] * nu, [1.0] * nu)
+            assert rel(U[b], U_ref) <= 1e-4, (N, b)
             assert abs(r["f"][b] - J) <= 1e-7 * max(1.0, abs(J)), (N, b)
             n_active += int(np.any(np.abs(U_ref) >= 1 - 1e-9))
         if N > 1:

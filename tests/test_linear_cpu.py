@@ -138,7 +138,7 @@ def test_box_qp_matches_active_set_enumeration():
         np.testing.assert_allclose(u, best[1], rtol=0, atol=1e-9, err_msg=str(trial))
 
 
-def _random_lin(rng, nx, nu=1, n_tab=3, N=12, B=None):
+def _random_lin(rng, nx, nu=1, n_tab=3, N=12, B=None, umax=1.0):
     from mpcx import lti
 
     nz = nx + nu
@@ -152,34 +152,36 @@ def _random_lin(rng, nx, nu=1, n_tab=3, N=12, B=None):
         Ws.append(M @ M.T / nz + 0.1 * np.eye(nz))
     tab = rng.integers(0, n_tab, size=(N,) if B is None else (B, N)).astype(np.int32)
     return lti.LinearOCP(N=N, A=np.stack(As), B=np.stack(Bs), c=np.stack(cs), W=np.stack(Ws), tab=tab,
-                         u_lb=(-1.0,), u_ub=(1.0,))
+                         u_lb=(-umax,) * nu, u_ub=(umax,) * nu)
 
 
-@pytest.mark.parametrize("nx", [1, 2, 3])
-def test_state_pad_embedding_same_optimum(nx):
+@pytest.mark.parametrize("nx,nu", [(1, 1), (2, 1), (3, 1), (2, 2), (3, 2)])
+def test_state_pad_embedding_same_optimum(nx, nu):
     """lti.StatePad (nx < 4, nu = 1 solved as the 4-state kernel model): the padded QP has the
     unpadded QP's optimum (LQ oracle on both, bounds active), the pad states stay 0, and the
     index maps round-trip every layout (w, P, g) with the pad entries where the kernel reads them."""
     from mpcx import lti
     from oracle import nlp_ref as R
 
-    rng = np.random.default_rng(10 + nx)
-    lin = _random_lin(rng, nx, N=12)
+    rng = np.random.default_rng(10 + nx + 7 * nu)
+    lin = _random_lin(rng, nx, nu=nu, N=12)
     pd = lti.state_pad(lin)
-    assert isinstance(pd, lti.StatePad) and pd.ocp.nx == 4 and pd.ocp.nu == 1
+    assert isinstance(pd, lti.StatePad) and pd.ocp.nx == 4 and pd.ocp.nu == nu
+    nzp = 4 + nu
     assert (pd.n_w, pd.n_p, pd.n_g) == (lin.n_w_ms, lin.n_p, lin.n_g_ms)
-    assert (pd.n_w_pad, pd.n_p_pad, pd.n_g_pad) == (4 + 5 * 12, 4 + 5 * 12, 4 * 13)
+    assert (pd.n_w_pad, pd.n_p_pad, pd.n_g_pad) == (4 + nzp * 12, 4 + nzp * 12, 4 * 13)
     assert np.all(np.isinf(pd.ocp.x_lb[nx:])) and np.all(np.isinf(pd.ocp.x_ub[nx:]))
     n_active = 0
     for b in range(6):
         x0 = 3.0 * rng.normal(size=nx)
-        zr = rng.normal(size=(lin.N, nx + 1))
+        zr = rng.normal(size=(lin.N, nx + nu))
         P = lin.params(x0, zr)
         Pp = pd.scatter(P, pd.p_idx, pd.n_p_pad)
-        x0p, zrp = Pp[0, :4], Pp[0, 4:].reshape(lin.N, 5)
+        x0p, zrp = Pp[0, :4], Pp[0, 4:].reshape(lin.N, nzp)
         assert np.all(x0p[nx:] == 0) and np.all(zrp[:, nx:4] == 0)
-        X, U, J = R.lq_solve(x0, lin.A, lin.B, lin.c, lin.W, lin.tab, zr, [-1.0], [1.0])
-        Xp, Up, Jp = R.lq_solve(x0p, pd.ocp.A, pd.ocp.B, pd.ocp.c, pd.ocp.W, pd.ocp.tab, zrp, [-1.0], [1.0])
+        lo, hi = [-1.0] * nu, [1.0] * nu
+        X, U, J = R.lq_solve(x0, lin.A, lin.B, lin.c, lin.W, lin.tab, zr, lo, hi)
+        Xp, Up, Jp = R.lq_solve(x0p, pd.ocp.A, pd.ocp.B, pd.ocp.c, pd.ocp.W, pd.ocp.tab, zrp, lo, hi)
         np.testing.assert_allclose(Up, U, rtol=0, atol=1e-10)
         np.testing.assert_allclose(Xp[:, :nx], X, rtol=0, atol=1e-10)
         assert np.all(Xp[:, nx:] == 0)
@@ -201,7 +203,8 @@ def test_state_pad_shapes():
     from mpcx import lti
 
     rng = np.random.default_rng(3)
-    assert lti.state_pad(_random_lin(rng, 4)) is None and lti.state_pad(_random_lin(rng, 5)) is None
-    for nx, nu in ((2, 2), (6, 1)):
+    for nx, nu in ((4, 1), (5, 1), (4, 2)):
+        assert lti.state_pad(_random_lin(rng, nx, nu=nu)) is None
+    for nx, nu in ((5, 2), (6, 1), (2, 3)):
         with pytest.raises(ValueError, match="instantiated"):
             lti.state_pad(_random_lin(rng, nx, nu=nu))
