@@ -14,6 +14,7 @@ tables: "free" stages (u_prev+ = u, cost on u - u_prev) and "blocked" stages
 Builders:
   * :func:`inverted_pendulum_qp` -- ``Inverted_pendulum/inverted_pendulum_single_shooting_mpctools.py:15-78``
   * :func:`lateral_ltv`          -- ``Trajectory Tracking/Trajectory_tracking_dynamic_model.py:13-145``
+  * :func:`lateral_error_lti`    -- ``Trajectory Tracking/Trajectory_tracking_le_LTI.py:17-79``
 """
 from __future__ import annotations
 
@@ -357,3 +358,111 @@ def lateral_ltv(N=10, Delta=0.05, vref=None, Q=(1.0, 1.0, 1.0, 1.0), R=1.0, delt
         tab = np.repeat(np.asarray(per_instance_tab, np.int32)[:, None], N, axis=1)
     return LinearOCP(N=N, A=np.stack(As), B=np.stack(Bs), W=Ws, tab=tab, T=Delta, u_lb=(-delta_max,),
                      u_ub=(delta_max,), name="lateral_ltv")
+
+
+# ----------------------------------------------------------------------------
+# Lateral-error LTI lane change (Trajectory Tracking/Trajectory_tracking_le_LTI.py)
+# ----------------------------------------------------------------------------
+
+def lateral_error_continuous(uref, ar=-23.55, br=61.99):
+    """``Trajectory_tracking_le_LTI.py:37-42``: states (y, phi, r), input delta."""
+    Ac = np.array([[0.0, uref, 0.0], [0.0, 0.0, 1.0], [0.0, 0.0, ar]])
+    Bc = np.array([[0.0], [0.0], [br]])
+    return Ac, Bc
+
+
+def lateral_error_lti(uref, N=5, n_free=1, Delta=0.05, q=(10.0, 1.0, 0.0), r=0.01, r_du=0.0, delta_max=0.3491,
+                      ar=-23.55, br=61.99, dummy_weight=1.0):
+    """The per-step QP of ``Trajectory_tracking_le_LTI.py:17-79``: ZOH model of (y, phi, r) at the
+    mean speed ``uref`` (:39-44), l = (x - p[:3])^T Q (x - p[:3]) + R (u - p[3])^2 + R_du Du^2
+    (:58-61), |u| <= delta_max (:69-73), Du free for the first n_free = Ntu moves and 0 after
+    (move blocking, :64-67), uprev = 0 (:79; the script never updates it).
+
+    As for the cart-pole QP, Du and move blocking become an augmented state x~ = (y, phi, r, u_prev)
+    (nx = 4, nu = 1): table 0 = free stage (u_prev+ = u, cost on u and u - u_prev), table 1 =
+    blocked stage (applied input = u_prev, cost R (u_prev - p[3])^2, the stage's own u a dummy held
+    at 0).  P = lateral_error_params(lin, x, u_prev, par_t).
+    """
+    Ac, Bc = lateral_error_continuous(uref, ar, br)
+    A, Bd = c2d(Ac, Bc, Delta)
+    Q = np.diag(np.asarray(q, float))
+    A0 = np.zeros((4, 4))
+    A0[:3, :3] = A
+    B0 = np.zeros((4, 1))
+    B0[:3] = Bd
+    B0[3, 0] = 1.0  # u_prev+ = u
+    A1 = np.zeros((4, 4))
+    A1[:3, :3] = A
+    A1[:3, 3] = Bd[:, 0]  # applied input = u_prev (Du = 0)
+    A1[3, 3] = 1.0
+    B1 = np.zeros((4, 1))
+    W0 = np.zeros((5, 5))
+    W0[:3, :3] = Q
+    W0[4, 4] = r + r_du
+    W0[3, 3] = r_du
+    W0[3, 4] = W0[4, 3] = -r_du  # R (u - ur)^2 + R_du (u - u_prev)^2, u_prev's reference = ur
+    W1 = np.zeros((5, 5))
+    W1[:3, :3] = Q
+    W1[3, 3] = r  # R (u_prev - ur)^2: the applied input of a blocked stage
+    W1[4, 4] = dummy_weight
+    tab = np.array([0 if k < n_free else 1 for k in range(N)], np.int32)
+    lin = LinearOCP(N=N, A=np.stack([A0, A1]), B=np.stack([B0, B1]), W=np.stack([W0, W1]), tab=tab, T=Delta,
+                    u_lb=(-delta_max,), u_ub=(delta_max,), name="lateral_error_lti")
+    lin.A_plant, lin.B_plant = A, Bd
+    lin.n_free = n_free
+    return lin
+
+
+def lateral_error_references(xref, yref, N=5, Delta=0.05, ar=-23.55, br=61.99):
+    """Per-(t, k) references p = (y_ref, phi_ref, r_ref, delta_ref) of
+    ``Trajectory_tracking_le_LTI.py:104-128`` for t = 0..len(xref)-1, as written: phi_ref from the
+    path's chord angle (0 at t + k = 0, the last chord past the end), r_ref and delta_ref by the
+    three finite-difference cases, which read the previous step's phi_ref of the same stage
+    (par[1, k, t-1]; the zero-initialised array at t = 0) and of stage k-1 (Python's index -1 =
+    the last stage at k = 0).  Returns par (Nsim, N, 4)."""
+    a, b = np.asarray(xref, float), np.asarray(yref, float)
+    Nsim = len(a)
+    par = np.zeros((Nsim, N, 4))
+    chord = lambda j: np.arctan2(b[j + 1] - b[j], a[j + 1] - a[j])  # noqa: E731
+    for t in range(Nsim):
+        prev = par[t - 1] if t > 0 else np.zeros((N, 4))  # par[:, :, -1] is still 0 at t = 0
+        for k in range(N):
+            p = np.zeros(4)
+            if t + k > Nsim - 1:
+                p[0] = b[Nsim - 1]
+                p[1] = chord(Nsim - 2)
+            elif t + k == 0:
+                p[0] = b[k + t]
+                p[1] = 0.0
+            else:
+                p[0] = b[k + t]
+                p[1] = chord(k + t - 1)
+            if t + k < 2:
+                phi_plus, phi_plus2 = chord(k + t), chord(k + t + 1)
+                p[2] = (phi_plus - p[1]) / Delta
+                p[3] = (((phi_plus2 - 2 * phi_plus + p[1]) / Delta ** 2) - ar * p[2]) / br
+            elif t + k > Nsim - 3:
+                p[2] = (p[1] - prev[k, 1]) / Delta
+                p[3] = (((p[1] - 2 * prev[k, 1] + prev[k - 1, 1]) / Delta ** 2) - ar * p[2]) / br
+            else:
+                phi_plus = chord(k + t)
+                p[2] = (phi_plus - prev[k, 1]) / (2 * Delta)
+                p[3] = (((phi_plus - 2 * p[1] + prev[k, 1]) / Delta ** 2) - ar * p[2]) / br
+            par[t, k] = p
+    return par
+
+
+def lateral_error_params(lin: LinearOCP, x, u_prev, par_t):
+    """P (B, n_p) of lateral_error_lti from x (B, 3), u_prev (B,) and the step's references
+    par_t (N, 4) or (B, N, 4): zr_k = (y_r, phi_r, r_r, delta_r, delta_r) on free stages (the
+    u_prev slot carries delta_r so that the Du term stays u - u_prev), (y_r, phi_r, r_r, delta_r, 0)
+    on blocked ones."""
+    x = np.atleast_2d(np.asarray(x, float))
+    Bn = x.shape[0]
+    par_t = np.broadcast_to(np.asarray(par_t, float), (Bn, lin.N, 4))
+    zr = np.zeros((Bn, lin.N, 5))
+    zr[:, :, :4] = par_t
+    free = lin.tab == 0 if lin.tab.ndim == 1 else lin.tab[0] == 0
+    zr[:, free, 4] = par_t[:, free, 3]
+    xt = np.concatenate([x, np.broadcast_to(np.asarray(u_prev, float), (Bn,))[:, None]], axis=1)
+    return lin.params(xt, zr)

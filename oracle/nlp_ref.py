@@ -596,6 +596,27 @@ def lq_solve(x0, A, B, c, W, tab, zr, lbu, ubu, x_lb=None, x_ub=None, tol=1e-13)
 # ----------------------------------------------------------------------------
 
 
+def lateral_error_solve(x0, A, Bd, par_t, q=(10.0, 1.0, 0.0), r=0.01, delta_max=0.3491):
+    """The per-step QP of ``Trajectory Tracking/Trajectory_tracking_le_LTI.py:17-79`` with its
+    settings Ntu = 1 (one free move: u_k = u_0 for every k, :64-67) and R_du = 0 (:28): a scalar
+    QP in u_0, J(u) = sum_{k<Nt} (x_k - p_k[:3])^T Q (x_k - p_k[:3]) + R (u - p_k[3])^2 with
+    x_{k+1} = A x_k + B u (:48-61), minimised in closed form and clamped to |u| <= delta_max
+    (:69-73).  Written independently of the augmented-state tables of mpcx.lti.  Returns
+    (u_0, x_1)."""
+    x0 = np.asarray(x0, float)
+    Q = np.diag(np.asarray(q, float))
+    b = np.asarray(Bd, float).reshape(-1)
+    h2 = h1 = 0.0
+    fx, sx = x0.copy(), np.zeros_like(x0)  # x_k = fx + sx u
+    for k in range(len(par_t)):
+        e = fx - par_t[k][:3]
+        h2 += sx @ Q @ sx + r
+        h1 += sx @ Q @ e - r * par_t[k][3]
+        fx, sx = A @ fx, A @ sx + b
+    u = float(np.clip(-h1 / h2, -delta_max, delta_max))
+    return u, A @ x0 + b * u
+
+
 def mpctools_point_to_point_ocp(N=10):
     """``mpctools/multiple_shooting_mpctools.py:9-70``: RK4 M=1 model (:51), node cost
     l = (x - goal)^T Q (x - goal) + u^T u (:57-58: R = I, the script's R is unused)."""

@@ -515,3 +515,39 @@ def test_padded_model_device_loop(mpcx, R):
         Pk = loop.P.cpu().numpy()
         np.testing.assert_allclose(Pk[:, 0:nx], x, rtol=1e-12, atol=1e-12)
         assert np.all(Pk[:, nx:4] == 0)
+
+
+def test_lateral_error_lti_closed_loop(mpcx, R):
+    """``Trajectory Tracking/Trajectory_tracking_le_LTI.py`` end to end: 500 steps of lane_change.csv
+    with the script's references (:104-128), one solve per step through the CasADi-shaped façade,
+    x_{t+1} = the solver's predicted x_1 (solver.fixvar, :145).  Every u_0 and x_1 against the
+    script's QP restated as a scalar QP (oracle.nlp_ref.lateral_error_solve).  The script keeps no
+    output, so parity is to the restatement only (unpinned)."""
+    import csv
+
+    from mpcx import lti
+
+    with open(os.path.join(ROOT, "tests", "golden", "lane_change.csv")) as f:
+        rows = list(csv.DictReader(f))
+    a, b, c = (np.array([float(r[k]) for r in rows]) for k in ("x", "y", "uref"))
+    lin = lti.lateral_error_lti(c.mean())
+    par = lti.lateral_error_references(a, b, N=lin.N)
+    S = mpcx.nlpsol("le_lti", "mi355x", lin, {"ipopt": {"max_iter": 200}})
+    lbx = np.full(S.n_w, -np.inf)
+    ubx = np.full(S.n_w, np.inf)
+    nz = 5
+    lbx[4::nz], ubx[4::nz] = -0.3491, 0.3491
+    x = np.zeros(3)
+    x_ref = np.zeros(3)
+    worst = 0.0
+    for t in range(len(a)):
+        sol = S(p=lti.lateral_error_params(lin, x, 0.0, par[t])[0], lbx=lbx, ubx=ubx)
+        assert S.stats()["success"], t
+        w = sol["x"][:, 0]
+        u_ref, x1_ref = R.lateral_error_solve(x_ref, lin.A_plant, lin.B_plant, par[t])
+        worst = max(worst, abs(w[4] - u_ref))
+        assert abs(w[4] - u_ref) <= 1e-4, t  # north-star bound (saturated steps sit O(sqrt(mu)) inside)
+        x = w[5:8]  # predicted x_1 (the script's fixvar)
+        x_ref = x1_ref
+        np.testing.assert_allclose(x, x_ref, rtol=0, atol=1e-3)
+    print(f"lateral-error LTI: 500 steps, max |u0 - u0_oracle| = {worst:.2e}")

@@ -208,3 +208,39 @@ def test_state_pad_shapes():
     for nx, nu in ((5, 2), (6, 1), (2, 3)):
         with pytest.raises(ValueError, match="instantiated"):
             lti.state_pad(_random_lin(rng, nx, nu=nu))
+
+
+def _lane_change():
+    import csv
+
+    with open(os.path.join(ROOT, "tests", "golden", "lane_change.csv")) as f:
+        rows = list(csv.DictReader(f))
+    return tuple(np.array([float(r[c]) for r in rows]) for c in ("x", "y", "uref"))
+
+
+def test_lateral_error_lti_tables_match_scalar_oracle():
+    """Trajectory_tracking_le_LTI.py: the augmented-state tables (Du, move blocking with Ntu = 1)
+    give, through the generic LQ oracle, the same u_0 as the script's QP restated as a scalar QP
+    (oracle.nlp_ref.lateral_error_solve), along the 500 closed-loop steps of lane_change.csv with the
+    script's references; x_{t+1} is the solver's predicted x_1 (solver.fixvar, :145)."""
+    from mpcx import lti
+    from oracle import nlp_ref as R
+
+    a, b, c = _lane_change()
+    lin = lti.lateral_error_lti(c.mean())
+    par = lti.lateral_error_references(a, b, N=lin.N)
+    assert par.shape == (500, 5, 4) and par[0, 0, 1] == 0.0
+    x = np.zeros(3)
+    n_sat = 0
+    for t in range(500):
+        u_ref, x1 = R.lateral_error_solve(x, lin.A_plant, lin.B_plant, par[t])
+        P = lti.lateral_error_params(lin, x, 0.0, par[t])[0]
+        xt0, zr = P[:4], P[4:].reshape(lin.N, 5)
+        X, U, _ = R.lq_solve(xt0, lin.A, lin.B, lin.c, lin.W, lin.tab, zr, [-0.3491], [0.3491])
+        assert abs(U[0, 0] - u_ref) <= 1e-9 * max(1.0, abs(u_ref)), t
+        np.testing.assert_allclose(X[1, :3], x1, rtol=0, atol=1e-12)
+        np.testing.assert_allclose(X[1:, 3], u_ref, rtol=0, atol=1e-9)  # u_prev carries u_0 (blocked moves)
+        n_sat += abs(u_ref) >= 0.3491 - 1e-12
+        x = x1
+    assert np.max(np.abs(par[:, :, 0])) > 1.0  # a lane change is tracked
+    assert abs(x[0] - par[-1, 0, 0]) < 0.2 * par[-1, 0, 0]  # and followed (final y 2.91 vs 2.77)
