@@ -15,6 +15,7 @@ Builders:
   * :func:`inverted_pendulum_qp` -- ``Inverted_pendulum/inverted_pendulum_single_shooting_mpctools.py:15-78``
   * :func:`lateral_ltv`          -- ``Trajectory Tracking/Trajectory_tracking_dynamic_model.py:13-145``
   * :func:`lateral_error_lti`    -- ``Trajectory Tracking/Trajectory_tracking_le_LTI.py:17-79``
+  * :func:`lateral_error_ltv`    -- ``Trajectory Tracking/Trjectory_tracking_le_LTV.py:27-166``
 """
 from __future__ import annotations
 
@@ -410,6 +411,20 @@ def lateral_error_lti(uref, N=5, n_free=1, Delta=0.05, q=(10.0, 1.0, 0.0), r=0.0
                     u_lb=(-delta_max,), u_ub=(delta_max,), name="lateral_error_lti")
     lin.A_plant, lin.B_plant = A, Bd
     lin.n_free = n_free
+    return lin
+
+
+def lateral_error_ltv(speed, N=5, n_free=1, Delta=0.05, **kw):
+    """The step-t QP of ``Trjectory_tracking_le_LTV.py``: the same construction as
+    :func:`lateral_error_lti` with the model rebuilt at the step's own speed c[t] (:130-136) and
+    that script's weights Q = diag(5, 0, 0), R = 0, R_du = 0 (:27-35).  The closed loop re-uploads
+    it every step (``solver.set_linear_model(lateral_error_ltv(c[t]))``) and sets
+    x0 = the simulated state (:165-166)."""
+    kw.setdefault("q", (5.0, 0.0, 0.0))
+    kw.setdefault("r", 0.0)
+    kw.setdefault("r_du", 0.0)
+    lin = lateral_error_lti(float(speed), N=N, n_free=n_free, Delta=Delta, **kw)
+    lin.name = "lateral_error_ltv"
     return lin
 
 

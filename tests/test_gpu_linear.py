@@ -551,3 +551,36 @@ def test_lateral_error_lti_closed_loop(mpcx, R):
         x_ref = x1_ref
         np.testing.assert_allclose(x, x_ref, rtol=0, atol=1e-3)
     print(f"lateral-error LTI: 500 steps, max |u0 - u0_oracle| = {worst:.2e}")
+
+
+def test_lateral_error_ltv_closed_loop(mpcx, R):
+    """``Trajectory Tracking/Trjectory_tracking_le_LTV.py``: the model rebuilt at every step's speed
+    c[t] (:130-136, tables re-uploaded through set_linear_model), Q = diag(5, 0, 0), R = 0 (:27-35),
+    x_{t+1} = the simulated state (:165-166; exact ZOH here).  500 steps against the scalar-QP
+    restatement; unpinned (the script keeps no output)."""
+    import csv
+
+    from mpcx import lti
+
+    with open(os.path.join(ROOT, "tests", "golden", "lane_change.csv")) as f:
+        rows = list(csv.DictReader(f))
+    a, b, c = (np.array([float(r[k]) for r in rows]) for k in ("x", "y", "uref"))
+    lin = lti.lateral_error_ltv(c[0])
+    par = lti.lateral_error_references(a, b, N=lin.N)
+    S = mpcx.nlpsol("le_ltv", "mi355x", lin, {"ipopt": {"max_iter": 300}})
+    lbx = np.full(S.n_w, -np.inf)
+    ubx = np.full(S.n_w, np.inf)
+    lbx[4::5], ubx[4::5] = -0.3491, 0.3491
+    x = np.zeros(3)
+    worst = 0.0
+    for t in range(len(a)):
+        lin_t = lti.lateral_error_ltv(c[t])
+        S.set_linear_model(lin_t)
+        sol = S(p=lti.lateral_error_params(lin_t, x, 0.0, par[t])[0], lbx=lbx, ubx=ubx)
+        assert S.stats()["success"], t
+        u0 = sol["x"][4, 0]
+        u_ref, _ = R.lateral_error_solve(x, lin_t.A_plant, lin_t.B_plant, par[t], q=(5.0, 0.0, 0.0), r=0.0)
+        worst = max(worst, abs(u0 - u_ref))
+        assert abs(u0 - u_ref) <= 1e-4, t
+        x = lin_t.A_plant @ x + lin_t.B_plant[:, 0] * u_ref  # the oracle's input drives both
+    print(f"lateral-error LTV: 500 steps, max |u0 - u0_oracle| = {worst:.2e}")
