@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: batched receding-horizon MPC solves on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]     (N > 1: starts its N ranks itself)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -310,12 +310,51 @@ def load_traffic(B, N):
     return None
 
 
+def launch_plan(gpus, env=None, n_devices=None):
+    """How `--gpus N` runs (decided before any GPU call).  Returns ("run", None) when this
+    process is one rank of a world of N, ("spawn", argv) when a plain `python bench.py --gpus N`
+    must start the N ranks itself (torch.distributed.run, one process per GPU, LOCAL_RANK ->
+    cuda:LOCAL_RANK), and raises SystemExit on any mismatch -- a line whose n_gpus differs
+    from --gpus is never printed."""
+    env = os.environ if env is None else env
+    if gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    under_launcher = "WORLD_SIZE" in env or "RANK" in env
+    world = int(env.get("WORLD_SIZE", "1"))
+    if under_launcher:
+        if world != gpus:
+            raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+                             f"(--nproc-per-node {gpus}) or drop the launcher")
+        return "run", None
+    if gpus == 1:
+        return "run", None
+    if n_devices is not None and gpus > n_devices and env.get("MPCX_FORCE_DEVICE") is None:
+        raise SystemExit(f"--gpus {gpus} but only {n_devices} visible GPU(s)")
+    import socket
+
+    with socket.socket() as so:  # a free rendezvous port on the loopback interface
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    argv = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return "spawn", argv
+
+
 def main():
     args = parse()
     from mpcx import dist as mdist
 
-    rank, world, local = mdist.env()
     import torch
+
+    # every rank check happens before the first GPU call (device_count does not initialise HIP)
+    plan, argv = launch_plan(args.gpus, n_devices=torch.cuda.device_count())
+    if plan == "spawn":
+        import subprocess
+
+        # the ranks run as child processes (never an exec from this process), rank 0 prints the line
+        raise SystemExit(subprocess.run(argv).returncode)
+    rank, world, local = mdist.env()
+    assert world == args.gpus
 
     local = mdist.device_index(local)
     torch.cuda.set_device(local)

@@ -120,8 +120,12 @@ typedef struct mpcx_spec {
      Casadi/multiple_shooting_casadi.py:188-196).  A field left 0 takes IPOPT's default:
      dual_inf_tol 1, constr_viol_tol 1e-4, compl_inf_tol 1e-4 (unscaled tests next to tol),
      acceptable_tol 1e-6, acceptable_dual_inf_tol 1e10, acceptable_constr_viol_tol 1e-2,
-     acceptable_compl_inf_tol 1e-2, acceptable_obj_change_tol 1e20, acceptable_iter 15
-     (-1 disables the acceptable-level termination). */
+     acceptable_compl_inf_tol 1e-2, acceptable_iter 15 (-1 disables the acceptable-level
+     termination).  acceptable_obj_change_tol is taken literally (IPOPT accepts 0); a NEGATIVE
+     value selects IPOPT's default 1e20.  mpcx_default_spec fills every field: the unicycle gets
+     the reference script's acceptable_tol 1e-8 / acceptable_obj_change_tol 1e-6 (the problem of
+     :181-197 as the script builds it), the ODE models IPOPT's defaults.  (mpcx.nlpsol without
+     options uses IPOPT's defaults for every model, as ca.nlpsol without options does.) */
   double dual_inf_tol, constr_viol_tol, compl_inf_tol;
   double acceptable_tol, acceptable_dual_inf_tol, acceptable_constr_viol_tol, acceptable_compl_inf_tol;
   double acceptable_obj_change_tol;
@@ -189,9 +193,13 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
                      const double* lam_x0, const double* lbw, const double* ubw, double* w_out, double* f_out,
                      double* g_out, double* lam_g, double* lam_x, int32_t* status, int32_t* iters);
 
-/* Device-pointer variant: no host synchronisation; all work is enqueued on
-   `stream` (a hipStream_t, NULL = default stream).  Any d_* except d_P and
-   d_w_out may be NULL. */
+/* Device-pointer variant: all work is enqueued on `stream` (a hipStream_t, NULL = default
+   stream).  Any d_* except d_P and d_w_out may be NULL.  The handle owns scratch buffers that
+   every launch of the handle uses (restoration workspace, cached suffix value functions), so a
+   handle must not be used on two streams concurrently (one handle per stream, as per thread).
+   The first call at a batch size larger than any before grows the restoration workspace: that
+   call waits for the device to go idle (an earlier launch may still read the old buffer) and is
+   therefore not capturable in a graph; later calls never synchronise. */
 int mpcx_solve_batch_dev(mpcx_handle* h, int32_t B, const double* d_P, const double* d_w0, const double* d_lam_g0,
                          const double* d_lam_x0, double* d_w_out, double* d_f_out, double* d_lam_g,
                          double* d_lam_x, int32_t* d_status, int32_t* d_iters, void* stream);

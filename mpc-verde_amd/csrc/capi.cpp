@@ -46,6 +46,7 @@ struct mpcx_handle {
   // decoupled-suffix value functions across launches (SolveArgs::pcache)
   double* d_pcache = nullptr;
   double pc_epoch = 0, pc_gen = 1;
+  double park_epoch = 0;  // solve launches with a restoration workspace (SolveArgs::park_flag)
 };
 
 namespace {
@@ -334,11 +335,12 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
   if (s->group_policy != 0 && s->group_policy != 1) return fail(MPCX_EINVAL, "group_policy must be 0 or 1");
   if (!(s->tol > 0)) return fail(MPCX_EINVAL, "tol must be > 0");
   {
-    const double o[8] = {s->dual_inf_tol, s->constr_viol_tol, s->compl_inf_tol, s->acceptable_tol,
-                         s->acceptable_dual_inf_tol, s->acceptable_constr_viol_tol, s->acceptable_compl_inf_tol,
-                         s->acceptable_obj_change_tol};
+    const double o[7] = {s->dual_inf_tol, s->constr_viol_tol, s->compl_inf_tol, s->acceptable_tol,
+                         s->acceptable_dual_inf_tol, s->acceptable_constr_viol_tol, s->acceptable_compl_inf_tol};
     for (double v : o)
       if (!(v >= 0)) return fail(MPCX_EINVAL, "IPOPT tolerance options must be >= 0 (0 = IPOPT default)");
+    if (std::isnan(s->acceptable_obj_change_tol))
+      return fail(MPCX_EINVAL, "acceptable_obj_change_tol is NaN (negative = IPOPT default)");
     if (s->acceptable_iter < -1) return fail(MPCX_EINVAL, "acceptable_iter must be >= -1");
     if (s->no_restoration != 0 && s->no_restoration != 1) return fail(MPCX_EINVAL, "no_restoration must be 0 or 1");
   }
@@ -509,7 +511,8 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
     a.acc_dual_inf_tol = d(sp.acceptable_dual_inf_tol, 1e10);
     a.acc_constr_viol_tol = d(sp.acceptable_constr_viol_tol, 1e-2);
     a.acc_compl_inf_tol = d(sp.acceptable_compl_inf_tol, 1e-2);
-    a.acc_obj_change_tol = d(sp.acceptable_obj_change_tol, 1e20);
+    // taken literally (0 included); negative = IPOPT's default
+    a.acc_obj_change_tol = sp.acceptable_obj_change_tol < 0 ? 1e20 : sp.acceptable_obj_change_tol;
     a.acc_iter = sp.acceptable_iter == 0 ? 15 : (sp.acceptable_iter < 0 ? 0 : sp.acceptable_iter);
     a.restoration = sp.no_restoration ? 0 : 1;
   }
@@ -542,26 +545,31 @@ static int solve_launch(mpcx_handle* h, mpcx::SolveArgs& a, hipStream_t stream) 
     const int G = mpcx::solve_group_size(a.N, a.B, a.n_simd, a.group_policy);
     const long bs = G > 64 ? G : 64;
     const long threads = ((long)a.B * G + bs - 1) / bs * bs;
-    const size_t need = (size_t)slots * threads;
+    const size_t need = (size_t)slots * threads + 1;  // + the park flag
     if (need > h->cap_ws) {
-      HIPCHK(hipDeviceSynchronize());
+      HIPCHK(hipDeviceSynchronize());  // a queued launch may still use the old buffer
       dev_free(h->d_ws);
       h->cap_ws = 0;
       HIPCHK(hipMalloc(&h->d_ws, need * sizeof(double)));
-      HIPCHK(hipMemset(h->d_ws, 0, need * sizeof(double)));  // no instance parked
+      // stream-ordered: the caller's stream may be non-blocking w.r.t. the null stream
+      HIPCHK(hipMemsetAsync(h->d_ws, 0, need * sizeof(double), stream));  // no instance parked
       h->cap_ws = need;
     }
     a.ws = h->d_ws;
     a.ws_stride = threads;
+    a.park_flag = h->d_ws + (size_t)slots * threads;
+    a.park_epoch = (h->park_epoch += 1);
   } else {
     a.restoration = 0;
   }
-  if (a.model == MPCX_MODEL_LINEAR && h->lin_dec != 0) {
-    // decoupled-suffix value functions of earlier launches (kernels.h "decoupled suffix")
+  // decoupled-suffix value functions of earlier launches (kernels.h "decoupled suffix").  Not
+  // with a caller-owned device schedule (mpcx_set_linear_tab_dev): the caller may rewrite it on
+  // the device between launches without a call the cache's generation could follow.
+  if (a.model == MPCX_MODEL_LINEAR && h->lin_dec != 0 && h->ext_tab == nullptr) {
     if (!h->d_pcache) {
       const size_t n = (size_t)(a.N + 2) * (a.nx * (a.nx + 1) / 2);
       HIPCHK(hipMalloc(&h->d_pcache, n * sizeof(double)));
-      HIPCHK(hipMemset(h->d_pcache, 0, n * sizeof(double)));  // header epoch 0: nothing cached
+      HIPCHK(hipMemsetAsync(h->d_pcache, 0, n * sizeof(double), stream));  // header epoch 0: nothing cached
     }
     a.pcache = h->d_pcache;
     a.pc_epoch = (h->pc_epoch += 1);

@@ -102,8 +102,8 @@ __device__ __forceinline__ int iuw(int k, int i) {
 // sum of log(slack) over the bounded components of a lane's variables as ONE log: the
 // product of the slacks' frexp mantissas (each in [0.5, 1), at most 2 NZ factors, so no
 // under/overflow) plus the exponents times ln 2.  One log instead of one per bound.
-template <int NZ>
-__device__ __forceinline__ double barrier_logsum(const double* z, const double* lb, const double* ub, const bool* hL,
+template <int NZ, class BL = const double*, class BU = const double*>
+__device__ __forceinline__ double barrier_logsum(const double* z, const BL& lb, const BU& ub, const bool* hL,
                                                  const bool* hU) {
   double m = 1.0;
   int e = 0;
@@ -197,6 +197,31 @@ namespace mpcx {
 // rarely taken branches: laid out away from the hot loop
 #define MPCX_COLD(c) __builtin_expect(!!(c), 0)
 
+// Model::kBoundsLds if the model declares it: the variable bounds of a lane live in LDS (its
+// column of a per-block buffer) instead of 2 NZ doubles of registers held through every phase
+template <class M, class = void>
+struct BoundsLdsOf {
+  static constexpr bool value = false;
+};
+template <class M>
+struct BoundsLdsOf<M, std::void_t<decltype(M::kBoundsLds)>> {
+  static constexpr bool value = M::kBoundsLds;
+};
+
+// read view of n doubles of a lane's LDS column (element i at p[i * S + off]).  relaunder()
+// makes the offset opaque to the compiler at a phase boundary, so loads of one phase are never
+// merged with (or hoisted into registers for) another phase: the values are re-read where used.
+template <int S>
+struct LdsCol {
+  const double* p;
+  int off;
+  __device__ __forceinline__ double operator[](int i) const { return p[i * S + off]; }
+  __device__ __forceinline__ void relaunder() { asm volatile("" : "+v"(off)); }
+};
+
+#ifndef MPCX_SOFT_INLINE
+#define MPCX_SOFT_INLINE true
+#endif
 #ifndef MPCX_WAVES_PER_EU
 #define MPCX_WAVES_ATTR
 #else
@@ -205,6 +230,9 @@ namespace mpcx {
 template <class Model, int G, bool RESUME = false>
 __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(SolveArgs a) {
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2, NP = NX * (NX + 1) / 2;
+  // resume launch: nothing parked by this step's solve launch -> return before any setup
+  if constexpr (RESUME)
+    if (*a.park_flag != a.park_epoch) return;
   static_assert(NP + NX <= kXchStride && 2 * NZ + NX <= kXchStride && NX * NX + NX <= kXchStride,
                 "LDS exchange slot too small");
   const int lane = threadIdx.x & 63;
@@ -245,31 +273,55 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   Model::load_ctx(ma, valid ? inst : 0, Pin, k, hasU, ctx);
 
   // ---- bounds of my variables z = (x_k, u_k); x_0 is free (pinned by g_0)
-  double lb[NZ], ub[NZ];
+  constexpr bool kBndLds = BoundsLdsOf<Model>::value;
+  __shared__ double bndbuf[kBndLds ? 2 * NZ * kSBS : 1];
+  double lb0[NZ], ub0[NZ];
   bool hL[NZ], hU[NZ];
 #pragma unroll
   for (int i = 0; i < NZ; ++i) {
-    lb[i] = -1e20;
-    ub[i] = 1e20;
+    lb0[i] = -1e20;
+    ub0[i] = 1e20;
   }
   if (hasX && k > 0)
     for (int i = 0; i < NX; ++i) {
-      lb[i] = a.lbw[ixw<NX, NU>(k, i)];
-      ub[i] = a.ubw[ixw<NX, NU>(k, i)];
+      lb0[i] = a.lbw[ixw<NX, NU>(k, i)];
+      ub0[i] = a.ubw[ixw<NX, NU>(k, i)];
     }
   if (hasU)
     for (int i = 0; i < NU; ++i) {
-      lb[NX + i] = a.lbw[iuw<NX, NU>(k, i)];
-      ub[NX + i] = a.ubw[iuw<NX, NU>(k, i)];
+      lb0[NX + i] = a.lbw[iuw<NX, NU>(k, i)];
+      ub0[NX + i] = a.ubw[iuw<NX, NU>(k, i)];
     }
   int nbnd_l = 0;
 #pragma unroll
   for (int i = 0; i < NZ; ++i) {
     const bool own = (i < NX) ? hasX : hasU;
-    hL[i] = own && lb[i] > -kInfBound;
-    hU[i] = own && ub[i] < kInfBound;
+    hL[i] = own && lb0[i] > -kInfBound;
+    hU[i] = own && ub0[i] < kInfBound;
     nbnd_l += (int)hL[i] + (int)hU[i];
   }
+  // lb / ub: registers, or (kBndLds) views of this lane's LDS column re-read in every phase
+  using BndT = std::conditional_t<kBndLds, LdsCol<kSBS>, const double*>;
+  BndT lb{}, ub{};
+  if constexpr (kBndLds) {
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+      bndbuf[i * kSBS + threadIdx.x] = lb0[i];
+      bndbuf[(NZ + i) * kSBS + threadIdx.x] = ub0[i];
+    }
+    lb = LdsCol<kSBS>{bndbuf, (int)threadIdx.x};
+    ub = LdsCol<kSBS>{bndbuf + NZ * kSBS, (int)threadIdx.x};
+  } else {
+    lb = lb0;
+    ub = ub0;
+  }
+  // a phase boundary: bound reads of the next phase are not merged with this one's
+  auto phase = [&]() __attribute__((always_inline)) {
+    if constexpr (kBndLds) {
+      lb.relaunder();
+      ub.relaunder();
+    }
+  };
   const double nbound = gsum<G>((double)nbnd_l, xw);
   // ---- decoupled suffix (linear models; riccati.h DEC).  On stages k >= kb every table is
   //      decoupled (B = 0, no x-u Hessian block) and no state is bounded, so with delta = 0
@@ -403,6 +455,12 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   // line search.
   constexpr bool kRes = RestoOf<Model>::value;
   const bool res_on = kRes && a.restoration != 0;  // kernel-uniform
+  // Models whose line search evaluates derivatives at its first trial (the unicycle) take IPOPT's
+  // soft restoration step in the solve loop (a cold block after the line search).  Only the
+  // restoration phase proper parks the instance for the resume launch, so an instance whose line
+  // search fails once does not serialise the rest of a multi-step launch.
+  constexpr bool kSoftInline = MPCX_SOFT_INLINE && kRes && Model::kEvalInSearch && !Model::kSOC;
+  bool soft_tried = false;  // this iteration's soft trial failed (the resume launch skips it)
   bool soft = false;
   int soft_count = 0;
   bool parked = false;       // left to the resume launch at a failed line search (solve launch)
@@ -578,8 +636,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       if (MPCX_COLD(__any(pending_rec))) {
         if (pending_rec) {
           pending_rec = false;
-          double* const wsl = a.ws + gid;
-          const long wst = a.ws_stride;
+          double* wsl = a.ws + gid;
+          long wst = a.ws_stride;
+          asm volatile("" : "+v"(wsl), "+v"(wst));  // no workspace addresses hoisted out of the loop
           auto W = [&](int i) __attribute__((always_inline)) -> double& { return wsl[(long)i * wst]; };
           constexpr int S = RestoWs::SC(NX, NZ);
           RecIO io;
@@ -593,6 +652,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           io.hasX = hasX;
           io.hasU = hasU;
           io.acc_now = W(S + RestoWs::sACCNOW) != 0.0;
+          io.soft_tried = W(S + RestoWs::sSOFTTRIED) != 0.0;
           io.tol = a.tol;
           io.mu_min = mu_min;
           io.fs = fs;
@@ -718,6 +778,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       theta_min = 1e-4 * fmax(1.0, theta0);
     }
     STAMP(0);
+    phase();
     // ------------------------------------------------------------ optimality error
     double ln[NX];
     group_next<G, NX>(lam, ln, xw);
@@ -801,6 +862,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     if (K > 1 && __all(done)) continue;
 
     STAMP(1);
+    phase();
     // ------------------------------------------------------------ barrier update
     // (IPOPT monotone update with mu_allow_fast_monotone_decrease: repeated while the barrier
     //  test holds; a tiny step forces the first decrease)
@@ -824,8 +886,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       if (!__any(dec)) break;
     }
     tiny_flag = false;
-
     STAMP(2);
+    phase();
     // ------------------------------------------------------------ barrier gradient, Sigma
     double sig[NZ], gp[NZ];
 #pragma unroll
@@ -846,6 +908,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     }
 
     STAMP(3);
+    phase();
     // ------------------------------------------------------------ Riccati + inertia correction
     double delta = 0.0;
     bool need = !done;  // instance still needs a factorisation
@@ -948,8 +1011,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
             mv(z[i], i);
             mv(zL[i], NZ + i);
             mv(zU[i], 2 * NZ + i);
-            mv(lb[i], 3 * NZ + i);
-            mv(ub[i], 4 * NZ + i);
+            mv(lb0[i], 3 * NZ + i);
+            mv(ub0[i], 4 * NZ + i);
           }
 #pragma unroll
           for (int i = 0; i < NX; ++i) mv(lam[i], 5 * NZ + i);
@@ -1096,6 +1159,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     riccati_gains<NX, NU>(fac, Kk, kfk);  // all lanes at once
 
     STAMP(4);
+    phase();
     // ------------------------------------------------------------ forward sweep: dw (lane k-1 -> k)
     // (a lambda: the second-order correction re-runs it with other right-hand sides)
     auto forward = [&](const double* cc_, const double* kf_, const double* pv_, const double* c0v_, double* dzo_,
@@ -1237,6 +1301,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     forward(cdef, kfk, pk, c0, dz, dlam);
 
     STAMP(5);
+    phase();
     // ------------------------------------------------------------ bound-dual step, fraction to boundary
     double amax_l = 1.0, az_l = 1.0, tiny_l = 0.0, gd_l = 0.0;
 #pragma unroll
@@ -1268,6 +1333,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     const double gd = gsum<G>(gd_l, xw);
 
     STAMP(6);
+    phase();
     // ------------------------------------------------------------ filter line search
     double thk_l = 0, phk_l = (hasU ? fs * qv : 0.0) - mu * barrier_logsum<NZ>(z, lb, ub, hL, hU);
 #pragma unroll
@@ -1281,6 +1347,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     tiny_flag = !done && tinystep;
     bool trial_fresh = false;  // accepted at the first trial, which evaluated derivatives
     bool lastrej_f = false;    // the last rejected trial passed the sufficient decrease test but not the filter
+    bool soft_pd = false;      // (kSoftInline) accepted by the primal-dual error reduction (filter kept)
+    soft_tried = false;
     // switching condition alpha (-gd)^s_phi > delta theta^s_theta  <=>  alpha > sw_a with
     // sw_a = delta theta^s_theta / (-gd)^s_phi -- also the third term of alpha_min; one exp of
     // logs, loop-invariant over the trials
@@ -1290,6 +1358,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     if constexpr (!Model::kSOC) {
     for (int ls = 0; ls < 80; ++ls) {
       if (!__any(searching)) break;
+      phase();
       double zt[NZ];
 #pragma unroll
       for (int i = 0; i < NZ; ++i) zt[i] = fma(alpha, dz[i], z[i]);  // the update's exact expression
@@ -1356,6 +1425,125 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         }
       }
     }
+    if constexpr (kSoftInline) {
+      // ---- IPOPT's soft restoration step (resto.h step 1), taken here, out of the hot path,
+      //      once the filter line search has failed or instead of it in the soft restoration
+      //      phase: primal and dual variables take the same step min(alpha_max, alpha_z),
+      //      accepted by the original criteria (the soft phase then ends) or by a reduction of
+      //      the barrier problem's primal-dual error by kSoftResto (the filter is left as it is);
+      //      at most kMaxSoftResto of them in a row.  Both primal-dual errors need derivatives,
+      //      at the current point (the failed search's first trial replaced them) and at the
+      //      trial point: ONE evaluation site run twice (no second copy of the model code).
+      const bool want = res_on && !done && !tinystep && !accepted;  // group-uniform
+      if (MPCX_COLD(__any(want))) {
+        bool go = false;
+        if (want) {
+          if (soft) {
+            go = ++soft_count <= kMaxSoftResto;
+          } else {
+            soft = true;
+            soft_count = 0;
+            go = true;
+          }
+          soft_tried = !go;
+          DIAG(12);
+        }
+        if (__any(go)) {
+          const double as = fmin(amax, az);
+          double zt[NZ], lt[NX];
+#pragma unroll
+          for (int i = 0; i < NZ; ++i) zt[i] = fma(as, dz[i], z[i]);
+#pragma unroll
+          for (int i = 0; i < NX; ++i) lt[i] = fma(as, dlam[i], lam[i]);
+          double pd[2] = {0.0, 0.0}, tht = 0.0, pht = 0.0;
+#pragma unroll 1
+          for (int e = 0; e < 2; ++e) {  // e = 0: current point, e = 1: trial point
+            double ze[NZ], le[NX], zLe[NZ], zUe[NZ];
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) {
+              ze[i] = e ? zt[i] : z[i];
+              zLe[i] = e ? fma(as, dzL[i], zL[i]) : zL[i];
+              zUe[i] = e ? fma(as, dzU[i], zU[i]) : zU[i];
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) le[i] = e ? lt[i] : lam[i];
+            eval_at(ze, le);
+            // primal-dual error of the barrier problem (resto.h pd_error: 1-norms, its order)
+            double lnx[NX], r[NZ];
+            group_next<G, NX>(le, lnx, xw);
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) r[i] = 0;
+            if (hasX) {
+#pragma unroll
+              for (int i = 0; i < NX; ++i) r[i] = gq[i] - le[i];
+              if (hasU) {
+#pragma unroll
+                for (int j = 0; j < NX; ++j)
+#pragma unroll
+                  for (int m = 0; m < NX; ++m)
+                    if (Model::AMASK & (1ull << (m * NX + j))) r[j] = fma(Model::jacA(ctx, A)[m * NX + j], lnx[m], r[j]);
+#pragma unroll
+                for (int l = 0; l < NU; ++l) {
+                  double acc = gq[NX + l];
+#pragma unroll
+                  for (int m = 0; m < NX; ++m)
+                    if (Model::BMASK & (1ull << (m * NU + l))) acc = fma(Model::jacB(ctx, Bm)[m * NU + l], lnx[m], acc);
+                  r[NX + l] = acc;
+                }
+              }
+            }
+            double pdl = 0.0, thl = 0.0;
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) {
+              pdl += fabs(r[i] + (zUe[i] - zLe[i]));
+              if (hL[i]) pdl += fabs((ze[i] - lb[i]) * zLe[i] - mu);
+              if (hU[i]) pdl += fabs((ub[i] - ze[i]) * zUe[i] - mu);
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+              pdl += fabs(cdef[i]) + fabs(c0[i]);
+              thl += fabs(cdef[i]) + fabs(c0[i]);
+            }
+            pd[e] = gsum<G>(pdl, xw);
+            if (e == 1) {
+              tht = gsum<G>(thl, xw);
+              pht = gsum<G>(fs * qv - mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU), xw);
+            }
+          }
+          fresh = false;  // the arrays hold the trial point's evaluation (kept if it is accepted)
+          const bool infilter = filt.contains(tht, pht, xw);
+          if (go) {
+            // the original criteria first ...
+            bool acc = isfinite(pht) && isfinite(tht) && tht <= theta_max;
+            bool ft = false;
+            if (acc) {
+              if (thk <= theta_min && gd < 0 && as > sw_a) {
+                acc = pht - phk <= kEtaPhi * as * gd + 10.0 * kEps * fabs(phk);
+                ft = acc;
+              } else {
+                acc = tht <= (1.0 - kGammaTheta) * thk || pht <= phk - kGammaPhi * thk + 10.0 * kEps * fabs(phk);
+              }
+            }
+            if (acc && !infilter) {  // a regular step: the soft phase ends
+              accepted = true;
+              ftype = ft;
+              lastrej_f = false;
+              soft = false;
+              soft_count = 0;
+            } else if (pd[1] <= kSoftResto * pd[0]) {  // ... then the primal-dual error reduction
+              accepted = true;
+              soft_pd = true;
+            } else {
+              soft_tried = true;
+            }
+            if (accepted) {
+              alpha = az = as;  // primal and dual variables take the same step
+              trial_fresh = true;
+            }
+          }
+        }
+      }
+    }
     } else {  // models with the second-order correction (their trials evaluate values only)
     // trial point zt: constraint violation, barrier objective, filter membership (group sums);
     // ct / ct0 receive the trial's own constraint values (interval k, and g_0 on lane 0)
@@ -1409,6 +1597,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     };
     for (int ls = 0; ls < 80; ++ls) {
       if (!__any(searching)) break;
+      phase();
       double zt[NZ];
 #pragma unroll
       for (int i = 0; i < NZ; ++i) zt[i] = fma(alpha, dz[i], z[i]);  // the update's exact expression
@@ -1608,12 +1797,19 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     //      recovers at the top of its next pass
     bool handled = false;
     if constexpr (kRes) {
-      const bool need_rec = res_on && !done && !tinystep && (soft || !accepted);
+      // (kSoftInline: the soft restoration step ran in the line search above; what is left is the
+      // restoration phase proper, which IPOPT enters unless the point is acceptable)
+      const bool need_rec = kSoftInline ? (res_on && !done && !tinystep && !accepted && !acceptable_now)
+                                        : (res_on && !done && !tinystep && (soft || !accepted));
       if (MPCX_COLD(__any(need_rec))) {
         if (need_rec) {
           DIAG(12);
-          double* const wsl = a.ws + gid;
-          const long wst = a.ws_stride;
+          // the workspace addresses are made opaque here, so that the compiler cannot hoist their
+          // computation out of the solve loop (45 loop-invariant 64-bit addresses held in
+          // registers through every iteration: +146 VGPR spills on the unicycle kernel)
+          double* wsl = a.ws + gid;
+          long wst = a.ws_stride;
+          asm volatile("" : "+v"(wsl), "+v"(wst));
           auto W = [&](int i) __attribute__((always_inline)) -> double& { return wsl[(long)i * wst]; };
 #pragma unroll
           for (int i = 0; i < NZ; ++i) {
@@ -1660,10 +1856,12 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           W(S + RestoWs::sAZ) = az;
           W(S + RestoWs::sSWA) = sw_a;
           W(S + RestoWs::sACCNOW) = acceptable_now ? 1.0 : 0.0;
+          W(S + RestoWs::sSOFTTRIED) = soft_tried ? 1.0 : 0.0;
           if constexpr (RESUME) {
             pending_rec = true;  // recovered at the top of the next pass
           } else {
             W(S + RestoWs::sPEND) = 1.0;  // left to the resume launch
+            *a.park_flag = a.park_epoch;   // (vector store; every parking lane writes the same value)
             done = parked = true;
           }
           handled = true;
@@ -1684,6 +1882,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     }
 
     STAMP(7);
+    phase();
     // ------------------------------------------------------------ update iterate
 #ifdef MPCX_DEBUG_PRINT
     if (inst == 0 && k == 0 && !done && !handled)
@@ -1691,12 +1890,13 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
              az, (int)ftype, mu, delta, thk, phk);
 #endif
     if (!done && !handled) {
-      if (!ftype) {  // augment the filter
+      if (!ftype && !soft_pd) {  // augment the filter (not after a soft step accepted by the pd error)
         if (filt.add((1.0 - kGammaTheta) * thk, phk - kGammaPhi * thk, k, xw)) DIAG(14);
       }
       // filter reset (IPOPT filter_reset_trigger = 5, max_filter_resets = 5): the filter is
       // cleared once the last rejection of 5 successive iterations was the filter's
-      if (lastrej_f) {
+      if (soft_pd) {
+      } else if (lastrej_f) {
         if (++frej >= kFilterResetTrigger && nfreset < kMaxFilterResets) {
           filt.clear();
           ++nfreset;
@@ -1724,6 +1924,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       }
     }
     STAMP(8);
+    phase();
   }
   STAMP(9);
 #ifdef MPCX_STAMPS

@@ -20,6 +20,12 @@
 #ifndef MPCX_PSCAN_UNICYCLE
 #define MPCX_PSCAN_UNICYCLE false
 #endif
+#ifndef MPCX_BOUNDS_LDS
+#define MPCX_BOUNDS_LDS false
+#endif
+#ifndef MPCX_UNICYCLE_RESTO
+#define MPCX_UNICYCLE_RESTO true
+#endif
 
 namespace mpcx {
 
@@ -37,6 +43,13 @@ struct UnicycleModel {
   // second-order correction (IPOPT max_soc): not here -- the first trial's evaluation replaces
   // the current point's derivatives, and config-2/3 solves do not reach it
   static constexpr bool kSOC = false;
+  // IPOPT's soft restoration and restoration phase (resto.h, the resume launch): a warm-started
+  // closed-loop solve that sits at its optimum to rounding level can fail the filter line
+  // search on noise in theta (tests/test_gpu_hard.py); IPOPT recovers it there
+  static constexpr bool kResto = MPCX_UNICYCLE_RESTO;
+  // variable bounds in LDS, re-read per phase (kernels.h LdsCol): removes the kernel's scratch
+  // spills but measured 1-2 % slower on config 2 (LDS latency on the line search), so off
+  static constexpr bool kBoundsLds = MPCX_BOUNDS_LDS;
   // backward Riccati recursion as a log-depth scan (pscan.h) instead of N dependent steps
   static constexpr bool kParallelRiccati = MPCX_PSCAN_UNICYCLE;
   struct Ctx {

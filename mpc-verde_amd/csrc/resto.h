@@ -144,6 +144,7 @@ struct RecIO {
   // in
   int it, max_iter, k, N, nw, ng;
   bool valid, hasX, hasU, acc_now;
+  bool soft_tried = false;  // the solve loop already took this iteration's soft step (kSoftInline)
   double tol, mu_min, fs, nbound, thk, phk, gd, amax, az, sw_a;
   // in / out
   double mu, tau, theta_max, theta_min, dw_last;
@@ -337,7 +338,9 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const
 
   // ======================================================= 1. soft restoration step
   bool try_soft = false;
-  if (io.soft) {
+  if (io.soft_tried) {
+    // the solve loop took (or, past kMaxSoftResto, declined) this iteration's soft step itself
+  } else if (io.soft) {
     if (++io.soft_count <= kMaxSoftResto) try_soft = true;
   } else {
     io.soft = true;

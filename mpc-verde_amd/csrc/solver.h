@@ -42,6 +42,10 @@ struct SolveArgs {
   int restoration;      // soft restoration + restoration phase on a failed line search (models with kResto)
   double* ws;           // restoration workspace: slot i of thread t at ws[i * ws_stride + t] (kResto models)
   long ws_stride;
+  // park flag (after the workspace): the solve launch stores park_epoch there when it parks an
+  // instance; a resume launch that finds another value returns at once (nothing to resume)
+  double* park_flag;
+  double park_epoch;
   // linear models with a decoupled suffix: P_k of the suffix stages as a launch of this handle
   // computed them at fs = 1, delta = 0 ((N + 1) x NP doubles, then the header {launch epoch,
   // table generation, kb}), or null; pc_epoch = this launch (> every earlier one), pc_gen = the
@@ -119,6 +123,7 @@ struct RestoWs {
     sPEND = 0,  // 1: the fast solve left this instance to the resume launch
     sFS, sMU, sTAU, sTHMAX, sTHMIN, sDWLAST, sFNEXT, sFN, sFREJ, sNFRESET, sACC, sFLAST,
     sSOFT, sSOFTN, sIT, sSTEP, sWARM, sTHK, sPHK, sGD, sAMAX, sAZ, sSWA, sACCNOW,
+    sSOFTTRIED,  // 1: the solve loop already took (and failed) this iteration's soft restoration step
     sFTH,                                      // this lane's filter slots (FilterLds<G>::S of kFilterMax)
     sFPH = sFTH + 16, kScalars = sFPH + 16
   };

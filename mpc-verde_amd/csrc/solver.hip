@@ -89,7 +89,7 @@ hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X,
 
 // restoration workspace per thread: the ODE models (kernels.h RestoWs); none elsewhere
 int resto_ws_slots(int model, int nx, int nu) {
-  if (model < 3 || model > 5) return 0;
+  if (model != 1 && (model < 3 || model > 5)) return 0;  // the models with kResto: unicycle (1), ODE (3-5)
   return RestoWs::slots(nx, nu);
 }
 

@@ -104,8 +104,11 @@ MODEL_IDS = {"unicycle": _lib.MODEL_UNICYCLE, "linear": _lib.MODEL_LINEAR, "kin_
 
 
 # IPOPT termination / recovery options the spec carries (IPOPT's names); values left out take
-# IPOPT's defaults, except the reference's own acceptable_tol / acceptable_obj_change_tol
-# (Casadi/multiple_shooting_casadi.py:192-193) for the unicycle scripts' problems
+# IPOPT's defaults for every model, as ca.nlpsol without options does.  The reference script
+# passes acceptable_tol 1e-8 / acceptable_obj_change_tol 1e-6 itself
+# (Casadi/multiple_shooting_casadi.py:188-196), and callers mirroring it pass them the same way;
+# the C ABI's mpcx_default_spec, which describes that script's problem, fills them in for the
+# unicycle (include/mpcx.h).
 IPOPT_OPTIONS = ("dual_inf_tol", "constr_viol_tol", "compl_inf_tol", "acceptable_tol", "acceptable_dual_inf_tol",
                  "acceptable_constr_viol_tol", "acceptable_compl_inf_tol", "acceptable_obj_change_tol",
                  "acceptable_iter")

@@ -12,6 +12,8 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def _free_port():
     s = socket.socket()
@@ -106,3 +108,36 @@ def test_config4_config5_inputs_shard_invariant():
     b = mdist.config5_inputs(10, 40)
     np.testing.assert_array_equal(a[10:], b)
     assert np.all(np.abs(a) <= [1, .5, .2, .5])
+
+
+def test_bench_gpus_flag_launch_plan():
+    """`--gpus N` is honoured: under a launcher the world size must equal N; a plain
+    `python bench.py --gpus N` starts N ranks itself through torch.distributed.run (loopback
+    rendezvous); a mismatch exits non-zero before any GPU call, so no line with another
+    n_gpus is ever printed."""
+    import bench
+
+    assert bench.launch_plan(1, env={}) == ("run", None)
+    assert bench.launch_plan(8, env={"WORLD_SIZE": "8", "RANK": "3"}) == ("run", None)
+    plan, argv = bench.launch_plan(4, env={}, n_devices=8)
+    assert plan == "spawn"
+    assert argv[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=4" in argv and "--master-addr=127.0.0.1" in argv
+    assert argv[7].endswith("bench.py")
+    for bad in (dict(gpus=4, env={"WORLD_SIZE": "2", "RANK": "0"}), dict(gpus=2, env={"WORLD_SIZE": "1", "RANK": "0"}),
+                dict(gpus=4, env={}, n_devices=1), dict(gpus=0, env={})):
+        with pytest.raises(SystemExit):
+            bench.launch_plan(**bad)
+    # one-GPU rehearsal of the multi-rank path (MPCX_FORCE_DEVICE): allowed past the device count
+    assert bench.launch_plan(2, env={"MPCX_FORCE_DEVICE": "0"}, n_devices=1)[0] == "spawn"
+
+
+def test_bench_gpus_mismatch_exits_nonzero():
+    import subprocess
+    import sys
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr and r.stdout == ""

@@ -437,6 +437,51 @@ def test_pendulum_suffix_cache_follows_table_changes(mpcx):
         assert np.max(np.abs(r["w"] - r1["w"])) > 1e-6  # the problems really differ
 
 
+def test_pendulum_suffix_cache_off_with_device_schedule(mpcx):
+    """A caller-owned device schedule (mpcx_set_linear_tab_dev, one row shared by the batch) may
+    be rewritten on the device between launches with no call the suffix cache's generation could
+    follow.  Here the rewrite keeps the suffix's first stage (kb = 5) but points the blocked
+    stages at a second blocked table with other weights: the result must equal a fresh handle of
+    the new schedule, bit for bit (the cross-launch cache is off for device schedules)."""
+    import ctypes
+
+    import torch
+
+    from mpcx import lti
+
+    N, B = 100, 64
+    rng = np.random.default_rng(8)
+    x = rng.uniform([-1, -.5, -.2, -.5], [1, .5, .2, .5], size=(B, 4))
+    l1 = lti.inverted_pendulum_qp(N=N)
+    l2 = lti.inverted_pendulum_qp(N=N, q=(1.5, 2.0))
+    A = np.concatenate([l1.A, l2.A[1:]])
+    Bm = np.concatenate([l1.B, l2.B[1:]])
+    W = np.concatenate([l1.W, l2.W[1:]])
+    sched1 = np.array([0] * 5 + [1] * (N - 5), np.int32)
+    sched2 = np.array([0] * 5 + [2] * (N - 5), np.int32)
+    mk = lambda tab: lti.LinearOCP(N=N, A=A, B=Bm, W=W, tab=tab, T=l1.T, u_lb=l1.u_lb, u_ub=l1.u_ub)  # noqa: E731
+    lin1 = mk(sched1)
+    lin1.x_target = l1.x_target
+    P = lti.pendulum_params(lin1, x, 0.0)
+    S = mpcx.nlpsol("dt", "mi355x", lin1, {"ipopt": {"max_iter": 200}})
+    dev = torch.from_numpy(sched1.copy()).cuda()
+    lib = mpcx._lib.load()
+    mpcx._lib.check(lib.mpcx_set_linear_tab_dev(S._h.ptr, ctypes.c_void_p(dev.data_ptr()), 1))
+    for _ in range(2):  # a cache, were it on, would be filled and then used here
+        r1 = S.solve_batch(P)
+    ref1 = mpcx.nlpsol("f1", "mi355x", mk(sched1), {"ipopt": {"max_iter": 200}}).solve_batch(P)
+    np.testing.assert_array_equal(r1["w"], ref1["w"])
+    dev.copy_(torch.from_numpy(sched2))  # in place, on the device: no library call
+    torch.cuda.synchronize()
+    r2 = S.solve_batch(P)
+    ref2 = mpcx.nlpsol("f2", "mi355x", mk(sched2), {"ipopt": {"max_iter": 200}}).solve_batch(P)
+    assert np.all(ref2["status"] == 0)
+    np.testing.assert_array_equal(r2["w"], ref2["w"])
+    np.testing.assert_array_equal(r2["iters"], ref2["iters"])
+    assert np.max(np.abs(r2["w"] - r1["w"])) > 1e-6  # the schedules really differ
+    mpcx._lib.check(lib.mpcx_set_linear_tab_dev(S._h.ptr, None, 0))
+
+
 def test_padded_double_integrator_closed_loop(mpcx, R):
     """A 2-state model (double integrator, no kernel instantiation of its own) through the
     CasADi-shaped call and the integrator, in the reference's closed-loop pattern

@@ -192,7 +192,7 @@ def test_dyn_bicycle_hardest_instances_are_kkt_points(mpcx):
     P = ocp.params(x0, refs)
     solver = mpcx.nlpsol("dyn", "mi355x", ocp, {"ipopt": {"max_iter": 3000}})
     r = solver.solve_batch(P)
-    assert np.mean(r["status"] == 0) >= 0.99, np.unique(r["status"], return_counts=True)
+    assert np.all(r["status"] <= 1), np.unique(r["status"], return_counts=True)
     assert r["iters"].max() < 250, r["iters"].max()
     pr = ode_ref.Problem(ocp)
     hard = [b for b in np.argsort(-r["iters"]) if r["status"][b] == 0][:6]

@@ -24,6 +24,7 @@ MAX_CONFIG2_MISMATCH = 0  # of 1024 config-2 instances
 MAX_HORIZON_MISMATCH = {}  # N -> allowed certified mismatches in test_horizons (none)
 MAX_FIXTURE_MISMATCH = 0  # of the 32 committed N=20 oracle optima (independent algorithm)
 MAX_ITER_MISMATCH = 0  # iteration counts vs the C++ IPOPT restatement, of 1024, cold and warm
+MAX_TRACKING_MISMATCH = 0  # of the 4096 config-3 tracking instances (round 3)
 
 
 def rel_err(a, b):
@@ -457,11 +458,13 @@ def test_device_loop_warm_matches_cold(mpcx, R, C):
 # ----------------------------------------------------------------------------- tracking (config 3 family)
 def test_tracking_vs_oracles(mpcx, R, C):
     """Trajectory_tracking.py's NLP (RK4 M=1, node cost, per-stage reference p_k, state
-    bounds) at config-3 sizes (N=30): GPU vs the C++ IPM oracle (same tol) and vs the
-    independent numpy oracle (tight tol; state bounds verified inactive there)."""
+    bounds) on the bench's own config-3 batch (N=30, B=4096, dist.config3_inputs): GPU vs the
+    C++ IPM oracle (same tol) instance by instance -- every differing optimum counted, KKT-
+    certified and no worse than the oracle's -- and vs the independent numpy oracle (tight tol;
+    state bounds verified inactive there)."""
     from mpcx import dist
 
-    N, B = 30, 256
+    N, B = 30, 4096
     tau0, P = dist.config3_inputs(0, B, N=N)
     ocp = mpcx.unicycle_tracking(N=N)
     solver = mpcx.nlpsol("trk", "mi355x", ocp)
@@ -474,7 +477,15 @@ def test_tracking_vs_oracles(mpcx, R, C):
     ref = C.solve_batch(rocp, x0, w0=R.join_w(X, np.zeros((B, N, 2))), pstage=ps)
     assert np.all(ref["status"] == 0)
     errs = np.array([rel_err(r["w"][b], ref["w"][b]) for b in range(B)])
-    assert np.mean(errs <= REL_TOL) >= 0.99, np.sort(errs)[-5:]
+    diff = np.flatnonzero(errs > REL_TOL)
+    n_it = int(np.sum(r["iters"] != ref["iters"]))
+    print(f"config 3 tracking: {diff.size} of {B} instances differ from the C++ oracle by > {REL_TOL:g} "
+          f"(max {errs.max():.2e}); {n_it} iteration counts differ")
+    assert diff.size <= MAX_TRACKING_MISMATCH, (diff, np.sort(errs)[-5:])
+    for b in diff:
+        pg, cv = R.kkt_residual_ms(r["w"][b], r["lam_g"][b], x0[b], rocp, pstage=ps[b])
+        assert pg <= KKT_CERT_TOL and cv <= KKT_CERT_TOL, (b, pg, cv)
+        assert r["f"][b] <= ref["f"][b] * (1 + 1e-9), (b, r["f"][b], ref["f"][b])
     tight = mpcx.nlpsol("trk", "mi355x", ocp, {"ipopt": {"tol": 1e-11}}).solve_batch(P[::32])
     for i, b in enumerate(range(0, B, 32)):
         U, Xs, info = R.solve_single_shooting(x0[b], rocp, pstage=ps[b])
@@ -778,16 +789,20 @@ def test_bench_two_ranks_rehearsal():
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     env = dict(os.environ, MPCX_FORCE_DEVICE="0", MPCX_DIST_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
-           "--warmup", "1", "--no-cpu", "--no-roofline"]
-    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert out.returncode == 0, out.stderr[-3000:]
-    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1  # rank 0 prints ONE line
-    d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * d["config"]["batch_per_gpu"]
-    assert d["failed_instances"] == 0 and d["value"] > 0 and d["steps"] == 3
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    flags = ["--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu", "--no-roofline"]
+    launched = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py")] + flags
+    plain = [sys.executable, os.path.join(ROOT, "bench.py")] + flags  # bench.py starts its 2 ranks itself
+    for cmd in (launched, plain):
+        out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+        assert out.returncode == 0, out.stderr[-3000:]
+        lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1  # rank 0 prints ONE line
+        d = json.loads(lines[0])
+        assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * d["config"]["batch_per_gpu"]
+        assert d["failed_instances"] == 0 and d["value"] > 0 and d["steps"] == 3
 
 
 def test_mpctools_variant_closed_loop_3exemplo(mpcx, R, golden):
