@@ -23,6 +23,9 @@
 #ifndef MPCX_BOUNDS_LDS
 #define MPCX_BOUNDS_LDS false
 #endif
+#ifndef MPCX_UNI_MOMENTS
+#define MPCX_UNI_MOMENTS true
+#endif
 #ifndef MPCX_UNICYCLE_RESTO
 #define MPCX_UNICYCLE_RESTO true
 #endif
@@ -74,7 +77,10 @@ struct UnicycleModel {
   __device__ __forceinline__ static void derivs(const ModelArgs& a, const Ctx& c, const double* z, const double* ln, double fs,
                                 double* xf, double& q, double* A, double* Bm, double* g, double* H) {
     const double u2[2] = {z[3], z[4]};
-    uni_derivs<true>(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H);
+    if constexpr (MPCX_UNI_MOMENTS)  // weighted-moment assembly (unicycle.h)
+      uni_derivs_moments(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H);
+    else
+      uni_derivs<true>(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H);
   }
   __device__ __forceinline__ static void value(const ModelArgs& a, const Ctx& c, const double* z, double* xf, double& q) {
     const double u2[2] = {z[3], z[4]};

@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "solver.h"
 #include "unicycle.h"
@@ -115,13 +116,21 @@ MPCX_DECLARE(cartpole)
 // horizons from which the unicycle's Riccati recursion runs as a log-depth scan (models.h
 // UnicycleScanModel): ceil(log2(N+1)) = 5 combine levels cost about as much as 25 chain steps
 constexpr int kUnicycleScanMinN = 25;
+// diagnostic knob: MPCX_UNICYCLE_SCAN_MIN_N overrides it (A/B of the two instantiations)
+static int unicycle_scan_min_n() {
+  static const int n = [] {
+    const char* e = getenv("MPCX_UNICYCLE_SCAN_MIN_N");
+    return e ? atoi(e) : kUnicycleScanMinN;
+  }();
+  return n;
+}
 
 // unicycle, the linear-model shapes the reference's QPs need (4x1 lateral / cart-pole, 5x1
 // cart-pole with the previous input as a state; 4x2 for two-input models), and the BASELINE's nonlinear ODE variants
 #define MPCX_DISPATCH(a, FN, ...)                                                 \
   do {                                                                            \
     if ((a).model == 1)                                                           \
-      return (a).N >= kUnicycleScanMinN ? FN##_unicycle_scan(__VA_ARGS__) : FN##_unicycle(__VA_ARGS__); \
+      return (a).N >= unicycle_scan_min_n() ? FN##_unicycle_scan(__VA_ARGS__) : FN##_unicycle(__VA_ARGS__); \
     if ((a).model == 2 && (a).nx == 4 && (a).nu == 1) return FN##_linear4(__VA_ARGS__); \
     if ((a).model == 2 && (a).nx == 5 && (a).nu == 1) return FN##_linear5(__VA_ARGS__); \
     if ((a).model == 2 && (a).nx == 4 && (a).nu == 2) return FN##_linear4x2(__VA_ARGS__); \

@@ -105,6 +105,165 @@ __device__ __forceinline__ void uni_value(const StageParams& sp, const double x[
   }
 }
 
+// Value, Jacobian and the exact Hessian of fs*q + lam^T xf, quadrature cost, by weighted moments.
+//
+// Every quadrature point p (weight w, angle offset tau) has Dx = xi_x + v a, Dy = xi_y + v b,
+// Dt = xi_t + tau w with xi = state - reference and (a, b, a1, b1, a2, b2) the partial sums of
+// the point; the derivatives of a, b w.r.t. (th, w) are -b, a / -b1, a1 (and of a1, b1 w.r.t. w:
+// -b2, a2).  Substituting Dx, Dy into the per-point gradient and Hessian terms (uni_derivs below)
+// leaves sums over the points of products of (a, b, a1, b1, a2, b2): 6 linear and 11 quadratic
+// weighted moments, accumulated with ~21 FMAs per point, and the gradient and Hessian are
+// assembled from them once per interval (the per-point formula costs ~90).  The value q keeps
+// the per-point sum of the quadratic cost, so the line search's objective is the same expression.
+__device__ __forceinline__ void uni_derivs_moments(const StageParams& sp, const double x[3], const double u[2],
+                                                   const double xr[3], const double ur[2], const double lam[3],
+                                                   double fs, double xf[3], double& q, double A[9], double Bm[6],
+                                                   double g[5], double H[15]) {
+  const double v = u[0], w = u[1], th = x[2];
+  const double h = sp.h, hh = 0.5 * h, h6 = h / 6.0, h3 = h / 3.0, third = 1.0 / 3.0;
+  const double xix = x[0] - xr[0], xiy = x[1] - xr[1], xit = th - xr[2];
+  // partial sums of the interval so far (position increments per unit speed, t- and t^2-moments)
+  double Ac = 0, As = 0, Ac1 = 0, As1 = 0, Ac2 = 0, As2 = 0;
+  // weighted moments over the quadrature points
+  double Sa = 0, Sb = 0, Sa1 = 0, Sb1 = 0, Sa2 = 0, Sb2 = 0;
+  double Saa = 0, Sbb = 0, Sab = 0, Saa1 = 0, Sbb1 = 0, Sab1 = 0, Sba1 = 0, Sa1a1 = 0, Sb1b1 = 0, Saa2 = 0, Sbb2 = 0;
+  double W0 = 0, Wt = 0, Wtt = 0;  // sum w, sum w tau, sum w tau^2
+  double qs = 0.0;
+  double s0, c0, sd, cd;
+  sincos(th, &s0, &c0);
+  sincos_small(hh * w, &sd, &cd);
+  // hh-scaled cos/sin of the substep's first angle and their t, t^2 multiples
+  double t0 = 0.0;
+  double u0 = hh * c0, v0 = hh * s0, u0t = 0.0, v0t = 0.0, u0tt = 0.0, v0tt = 0.0;
+  auto point = [&](double a, double b, double a1, double b1, double a2, double b2, double tau, double wt)
+                   __attribute__((always_inline)) {
+    const double Dx = fma(v, a, xix), Dy = fma(v, b, xiy), Dt = fma(tau, w, xit);
+    qs = fma(wt, fma(sp.Q[0] * Dx, Dx, fma(sp.Q[1] * Dy, Dy, sp.Q[2] * Dt * Dt)), qs);
+    const double aw = wt * a, bw = wt * b, a1w = wt * a1, b1w = wt * b1;
+    Sa += aw;
+    Sb += bw;
+    Sa1 += a1w;
+    Sb1 += b1w;
+    Sa2 = fma(wt, a2, Sa2);
+    Sb2 = fma(wt, b2, Sb2);
+    Saa = fma(aw, a, Saa);
+    Sbb = fma(bw, b, Sbb);
+    Sab = fma(aw, b, Sab);
+    Saa1 = fma(aw, a1, Saa1);
+    Sbb1 = fma(bw, b1, Sbb1);
+    Sab1 = fma(aw, b1, Sab1);
+    Sba1 = fma(bw, a1, Sba1);
+    Sa1a1 = fma(a1w, a1, Sa1a1);
+    Sb1b1 = fma(b1w, b1, Sb1b1);
+    Saa2 = fma(aw, a2, Saa2);
+    Sbb2 = fma(bw, b2, Sbb2);
+    W0 += wt;
+    Wt = fma(wt, tau, Wt);
+    Wtt = fma(wt * tau, tau, Wtt);
+  };
+  for (int m = 0; m < sp.M; ++m) {
+    const double tm = t0 + hh, te = t0 + h;
+    const double c1 = c0 * cd - s0 * sd, s1 = s0 * cd + c0 * sd;
+    const double c2 = c1 * cd - s1 * sd, s2 = s1 * cd + c1 * sd;
+    const double u1 = hh * c1, v1 = hh * s1, u1t = tm * u1, v1t = tm * v1, u1tt = tm * u1t, v1tt = tm * v1t;
+    const double u2 = hh * c2, v2 = hh * s2, u2t = te * u2, v2t = te * v2, u2tt = te * u2t, v2tt = te * v2t;
+    if (sp.cost == 0) {
+      // RK4 stage points: (x, th_0), (x + hh f(th_0), th_1), (x + hh f(th_1), th_1), (x + h f(th_1), th_2)
+      point(Ac, As, Ac1, As1, Ac2, As2, t0, h6);
+      point(Ac + u0, As + v0, Ac1 + u0t, As1 + v0t, Ac2 + u0tt, As2 + v0tt, tm, h3);
+      point(Ac + u1, As + v1, Ac1 + u1t, As1 + v1t, Ac2 + u1tt, As2 + v1tt, tm, h3);
+      point(fma(2.0, u1, Ac), fma(2.0, v1, As), fma(2.0, u1t, Ac1), fma(2.0, v1t, As1), fma(2.0, u1tt, Ac2),
+            fma(2.0, v1tt, As2), te, h6);
+    }
+    // Simpson: h6 (f0 + 4 f1 + f2) = (u0 + 4 u1 + u2) / 3 in hh-scaled terms
+    Ac = fma(third, fma(4.0, u1, u0 + u2), Ac);
+    As = fma(third, fma(4.0, v1, v0 + v2), As);
+    Ac1 = fma(third, fma(4.0, u1t, u0t + u2t), Ac1);
+    As1 = fma(third, fma(4.0, v1t, v0t + v2t), As1);
+    Ac2 = fma(third, fma(4.0, u1tt, u0tt + u2tt), Ac2);
+    As2 = fma(third, fma(4.0, v1tt, v0tt + v2tt), As2);
+    c0 = c2;
+    s0 = s2;
+    u0 = u2;
+    v0 = v2;
+    u0t = u2t;
+    v0t = v2t;
+    u0tt = u2tt;
+    v0tt = v2tt;
+    t0 = te;
+  }
+  const double T = sp.T;
+  xf[0] = x[0] + v * Ac;
+  xf[1] = x[1] + v * As;
+  xf[2] = th + T * w;
+  A[0] = 1.0; A[1] = 0.0; A[2] = -v * As;
+  A[3] = 0.0; A[4] = 1.0; A[5] = v * Ac;
+  A[6] = 0.0; A[7] = 0.0; A[8] = 1.0;
+  Bm[0] = Ac; Bm[1] = -v * As1;
+  Bm[2] = As; Bm[3] = v * Ac1;
+  Bm[4] = 0.0; Bm[5] = T;
+  const double dv = u[0] - ur[0], dw = u[1] - ur[1];
+  const double Cx = 2.0 * fs * sp.Q[0], Cy = 2.0 * fs * sp.Q[1], Ct = 2.0 * fs * sp.Q[2];
+  const double lx = lam[0], ly = lam[1];
+  if (sp.cost != 0) {  // node cost (mpctools, Trajectory_tracking.py:51-61): l(x_k, u_k, p_k)
+    q = sp.Q[0] * xix * xix + sp.Q[1] * xiy * xiy + sp.Q[2] * xit * xit + sp.R[0] * dv * dv + sp.R[1] * dw * dw;
+    g[0] = Cx * xix;
+    g[1] = Cy * xiy;
+    g[2] = Ct * xit;
+    g[3] = 2.0 * sp.R[0] * fs * dv;
+    g[4] = 2.0 * sp.R[1] * fs * dw;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) H[i] = 0.0;
+    H[hix(0, 0)] = Cx;
+    H[hix(1, 1)] = Cy;
+    H[hix(2, 2)] = Ct - v * (lx * Ac + ly * As);
+    H[hix(3, 3)] = 2.0 * sp.R[0] * fs;
+    H[hix(4, 4)] = 2.0 * sp.R[1] * fs - v * (lx * Ac2 + ly * As2);
+    H[hix(2, 3)] = ly * Ac - lx * As;
+    H[hix(2, 4)] = -v * (lx * Ac1 + ly * As1);
+    H[hix(3, 4)] = ly * Ac1 - lx * As1;
+    return;
+  }
+  q = qs + T * (sp.R[0] * dv * dv + sp.R[1] * dw * dw);
+  // gradient and Hessian of fs q (C = 2 fs Q) from the moments
+  const double Xa = fma(v, Saa, xix * Sa), Xb = fma(v, Sab, xix * Sb);     // sum w Dx a, sum w Dx b
+  const double Ya = fma(v, Sab, xiy * Sa), Yb = fma(v, Sbb, xiy * Sb);     // sum w Dy a, sum w Dy b
+  const double Xa1 = fma(v, Saa1, xix * Sa1), Xb1 = fma(v, Sab1, xix * Sb1);
+  const double Ya1 = fma(v, Sba1, xiy * Sa1), Yb1 = fma(v, Sbb1, xiy * Sb1);
+  const double Xa2 = fma(v, Saa2, xix * Sa2), Yb2 = fma(v, Sbb2, xiy * Sb2);
+  const double Tsum = fma(w, Wt, xit * W0), Ttau = fma(w, Wtt, xit * Wt);  // sum w Dt, sum w Dt tau
+  const double vv = v * v;
+  g[0] = Cx * fma(v, Sa, xix * W0);
+  g[1] = Cy * fma(v, Sb, xiy * W0);
+  g[2] = fma(v, Cy * Ya - Cx * Xb, Ct * Tsum);
+  g[3] = fma(Cx, Xa, Cy * Yb);
+  g[4] = fma(v, Cy * Ya1 - Cx * Xb1, Ct * Ttau);
+  H[hix(0, 0)] = Cx * W0;
+  H[hix(0, 1)] = 0.0;
+  H[hix(0, 2)] = -v * (Cx * Sb);
+  H[hix(0, 3)] = Cx * Sa;
+  H[hix(0, 4)] = -v * (Cx * Sb1);
+  H[hix(1, 1)] = Cy * W0;
+  H[hix(1, 2)] = v * (Cy * Sa);
+  H[hix(1, 3)] = Cy * Sb;
+  H[hix(1, 4)] = v * (Cy * Sa1);
+  H[hix(2, 2)] = fma(vv, fma(Cx, Sbb, Cy * Saa), fma(-v, fma(Cx, Xa, Cy * Yb), Ct * W0));
+  H[hix(2, 3)] = fma(v * Sab, Cy - Cx, Cy * Ya - Cx * Xb);
+  H[hix(2, 4)] = fma(vv, fma(Cx, Sbb1, Cy * Saa1), fma(-v, fma(Cx, Xa1, Cy * Yb1), Ct * Wt));
+  H[hix(3, 3)] = fma(Cx, Saa, Cy * Sbb);
+  H[hix(3, 4)] = fma(v, Cy * Sba1 - Cx * Sab1, Cy * Ya1 - Cx * Xb1);
+  H[hix(4, 4)] = fma(vv, fma(Cx, Sb1b1, Cy * Sa1a1), fma(-v, fma(Cx, Xa2, Cy * Yb2), Ct * Wtt));
+  g[3] += 2.0 * T * sp.R[0] * fs * dv;
+  g[4] += 2.0 * T * sp.R[1] * fs * dw;
+  H[hix(3, 3)] += 2.0 * T * sp.R[0] * fs;
+  H[hix(4, 4)] += 2.0 * T * sp.R[1] * fs;
+  H[hix(2, 2)] -= v * (lx * Ac + ly * As);
+  H[hix(2, 3)] += ly * Ac - lx * As;
+  H[hix(2, 4)] -= v * (lx * Ac1 + ly * As1);
+  H[hix(3, 4)] += ly * Ac1 - lx * As1;
+  H[hix(4, 4)] -= v * (lx * Ac2 + ly * As2);
+}
+
 // Value, Jacobian and (if WANT_H) the exact Hessian of fs*q + lam^T xf.
 //   A (3x3 row-major) = dxf/dx, Bm (3x2) = dxf/du, g (5) = fs * dq/dz,
 //   H (15 packed) = fs * d2q/dz2 + sum_c lam_c d2xf_c/dz2.

@@ -1,0 +1,89 @@
+"""The unicycle stage derivatives of the solve kernel (mpc-verde_amd/csrc/unicycle.h) through the
+device harness tests/hip/stage_check.hip: the weighted-moment assembly the kernel uses
+(uni_derivs_moments) against the per-point formula (uni_derivs) on the device, and both against
+the C++ oracle's jets (oracle/ipm_ref.cpp oracle_stage: interval map, Jacobian, gradient of q and
+the exact Hessian of q + lam^T xf), for the quadrature cost (Casadi/multiple_shooting_casadi.py:
+98-114, M = 4) and the node cost (Trajectory_tracking.py:51-61, M = 1).
+
+Tolerances: the two device formulas <= 1e-12 relative to the entry's scale (they sum the same
+terms in another order); device vs oracle <= 1e-11 relative to the largest entry of its block.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hip", "libstage_check.so")
+
+
+@pytest.fixture(scope="module")
+def harness():
+    import torch  # noqa: F401  (its HIP runtime first: the harness must bind to the same one)
+
+    if not os.path.exists(LIB):
+        pytest.fail(f"{LIB} not built (make -C tests/hip)")
+    lib = ctypes.CDLL(LIB)
+    dp = ctypes.c_void_p
+    lib.stage_check.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(ctypes.c_double), dp, dp, dp, dp, dp, ctypes.c_double, dp]
+    return lib
+
+
+def run(harness, n, T, M, cost, Q, R, X, U, XR, UR, L, fs):
+    import torch
+
+    dev = [torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda() for a in (X, U, XR, UR, L)]
+    out = torch.zeros(2 * n * 39, dtype=torch.float64, device="cuda")
+    q = (ctypes.c_double * 3)(*Q)
+    r = (ctypes.c_double * 2)(*R)
+    rc = harness.stage_check(n, T, M, cost, q, r, *[ctypes.c_void_p(t.data_ptr()) for t in dev], fs,
+                             ctypes.c_void_p(out.data_ptr()))
+    assert rc == 0
+    o = out.cpu().numpy().reshape(2, n, 39)
+    return o[0], o[1]
+
+
+def blocks(o):
+    return {"xf": o[:, 0:3], "q": o[:, 3:4], "A": o[:, 4:13], "B": o[:, 13:19], "g": o[:, 19:24], "H": o[:, 24:39]}
+
+
+@pytest.mark.parametrize("cost,M", [(0, 4), (0, 1), (0, 7), (1, 1)])
+def test_moment_assembly_equals_per_point_formula_and_oracle(harness, cost, M):
+    from oracle import ipm_ref, nlp_ref
+
+    rng = np.random.default_rng(10 + M + cost)
+    n = 4096
+    T = 0.2
+    Q, R = (1.0, 5.0, 0.1), (0.5, 0.05)
+    X = np.column_stack([rng.uniform(-10, 10, n), rng.uniform(-10, 10, n), rng.uniform(-4, 4, n)])
+    U = np.column_stack([rng.uniform(-1, 1, n), rng.uniform(-np.pi / 4, np.pi / 4, n)])
+    XR = np.column_stack([rng.uniform(-10, 10, n), rng.uniform(-10, 10, n), rng.uniform(-4, 4, n)])
+    UR = np.column_stack([rng.uniform(-1, 1, n), rng.uniform(-1, 1, n)]) if cost == 1 else np.zeros((n, 2))
+    L = rng.normal(size=(n, 3)) * 5
+    # degenerate rows: standing still, at the reference, zero rotation
+    X[:8] = XR[:8]
+    U[:4, 0] = 0.0
+    U[4:8, 1] = 0.0
+    mom, pp = (blocks(o) for o in run(harness, n, T, M, cost, Q, R, X, U, XR, UR, L, 1.0))
+    for name in mom:
+        scale = np.maximum(np.max(np.abs(pp[name]), axis=1, keepdims=True), 1.0)
+        err = np.max(np.abs(mom[name] - pp[name]) / scale)
+        assert err <= 1e-12, (name, err)
+    # the C++ oracle (jets): fs = 1
+    ocp = nlp_ref.UnicycleOCP(N=1, M=M)
+    ocp.cost = "quadrature" if cost == 0 else "node"
+    xf, qf, jac, hess = ipm_ref.stage(ocp, X, U, XR, UR if cost == 1 else None, L)
+    ref = {"xf": xf, "q": qf[:, None], "A": jac[:, 0:3, 0:3].reshape(n, 9), "B": jac[:, 0:3, 3:5].reshape(n, 6),
+           "g": jac[:, 3, :], "H": hess}
+    for name in mom:
+        scale = max(1.0, float(np.max(np.abs(ref[name]))))
+        err = float(np.max(np.abs(mom[name] - ref[name]))) / scale
+        assert err <= 1e-11, (name, err)
+    # objective scaling fs: g and H scale (the lam^T xf part of H does not)
+    mom2 = blocks(run(harness, n, T, M, cost, Q, R, X, U, XR, UR, np.zeros_like(L), 0.25)[0])
+    mom1 = blocks(run(harness, n, T, M, cost, Q, R, X, U, XR, UR, np.zeros_like(L), 1.0)[0])
+    np.testing.assert_allclose(mom2["g"], 0.25 * mom1["g"], rtol=1e-13, atol=1e-13)
+    np.testing.assert_allclose(mom2["H"], 0.25 * mom1["H"], rtol=1e-13, atol=1e-13)
