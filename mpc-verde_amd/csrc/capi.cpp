@@ -47,6 +47,7 @@ struct mpcx_handle {
   double* d_pcache = nullptr;
   double pc_epoch = 0, pc_gen = 1;
   double park_epoch = 0;  // solve launches with a restoration workspace (SolveArgs::park_flag)
+  int spec_xbnd = 1;      // the spec bounds bound some state (SolveArgs::xbnd)
 };
 
 namespace {
@@ -141,6 +142,16 @@ void spec_bounds(const mpcx_spec& s, std::vector<double>& lb, std::vector<double
       ub[nx + nz * k + nu + i] = s.ubx[i];
     }
   }
+}
+
+// 1 if any node k >= 1 has a finite state bound (X_0 is always free)
+int state_bounded(const std::vector<double>& lb, const std::vector<double>& ub, int nx, int nu, int N) {
+  for (int k = 1; k <= N; ++k)
+    for (int i = 0; i < nx; ++i) {
+      const int j = nx + (nx + nu) * (k - 1) + nu + i;
+      if (lb[j] > -1e19 || ub[j] < 1e19) return 1;
+    }
+  return 0;
 }
 
 // Device buffers are released by the helpers below, which also null the pointers: a failed
@@ -369,6 +380,7 @@ int mpcx_create(const mpcx_spec* s, mpcx_handle** out) {
   h->np = s->param_layout == MPCX_P_X0_XREF ? 2 * nx : nx + nz * s->N;
   std::vector<double> lb, ub;
   spec_bounds(*s, lb, ub);
+  h->spec_xbnd = state_bounded(lb, ub, h->spec.nx, h->spec.nu, s->N);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&h->d_lbw, h->nw * sizeof(double)) != hipSuccess ||
       hipMalloc(&h->d_ubw, h->nw * sizeof(double)) != hipSuccess ||
@@ -528,6 +540,7 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
   a.mult_push = h->spec.warm_mult_push;
   a.lbw = lbw;
   a.ubw = ubw;
+  a.xbnd = h->spec_xbnd;
   a.w_out = w;
   a.f_out = f;
   a.lam_out = lam;
@@ -658,6 +671,7 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
   hipStream_t s = h->stream;
   const double* dl = h->d_lbw;
   const double* du = h->d_ubw;
+  int call_xbnd = h->spec_xbnd;
   if (lbw || ubw) {
     std::vector<double> lb, ub;
     spec_bounds(h->spec, lb, ub);
@@ -676,6 +690,7 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
     HIPCHK(hipStreamSynchronize(s));
     dl = h->d_lbw_call;
     du = h->d_ubw_call;
+    call_xbnd = state_bounded(lb, ub, h->spec.nx, h->spec.nu, h->spec.N);
   }
   HIPCHK(hipMemcpyAsync(h->d_P, P, (size_t)B * h->np * sizeof(double), hipMemcpyHostToDevice, s));
   if (w0) HIPCHK(hipMemcpyAsync(h->d_w0, w0, (size_t)B * h->nw * sizeof(double), hipMemcpyHostToDevice, s));
@@ -684,6 +699,7 @@ int mpcx_solve_batch(mpcx_handle* h, int32_t B, const double* P, const double* w
   mpcx::SolveArgs a = make_args(h, B, h->d_P, w0 ? h->d_w0 : nullptr, lam_g0 ? h->d_lam0 : nullptr,
                                 lam_x0 ? h->d_lamx0 : nullptr, dl, du, h->d_w, h->d_f, (lam_g ? h->d_lam : nullptr),
                                 (lam_x ? h->d_lamx : nullptr), h->d_status, h->d_iters);
+  a.xbnd = call_xbnd;
   if (int r = solve_launch(h, a, s)) return r;
   if (lam_x) HIPCHK(hipMemcpyAsync(lam_x, h->d_lamx, (size_t)B * h->nw * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(w_out, h->d_w, (size_t)B * h->nw * sizeof(double), hipMemcpyDeviceToHost, s));

@@ -44,14 +44,36 @@ __device__ __forceinline__ Pair halves32(double v) {
           __longlong_as_double(((long long)hi[1] << 32) | (unsigned int)lo[1])};
 }
 
+// max / min of doubles that are never signalling NaNs -- every value of the solve loop is an
+// arithmetic result, a DPP/permlane copy of one or a load of one -- as the bare v_max_f64 /
+// v_min_f64.  LLVM's fmax/fmin must first quiet each operand it cannot prove quiet (a
+// `v_max_f64 x, x` per DPP-moved, loaded or |.|-modified operand: 229 of the config-2 kernel's
+// 404 v_max_f64); the instruction's result for quiet NaNs and numbers is the same.
+__device__ __forceinline__ double qmax(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double qmin(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// max(a, |b|) with the abs source modifier
+__device__ __forceinline__ double qmax_abs(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, |%2|" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 struct OpSum {
   __device__ static double f(double a, double b) { return a + b; }
 };
 struct OpMax {
-  __device__ static double f(double a, double b) { return fmax(a, b); }
+  __device__ static double f(double a, double b) { return qmax(a, b); }
 };
 struct OpMin {
-  __device__ static double f(double a, double b) { return fmin(a, b); }
+  __device__ static double f(double a, double b) { return qmin(a, b); }
 };
 
 // Groups wider than a wavefront (G = 128 / 256: horizons N >= 64) span G/64 waves of one

@@ -282,7 +282,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     lb0[i] = -1e20;
     ub0[i] = 1e20;
   }
-  if (hasX && k > 0)
+  if (XBoundsOf<Model>::value && hasX && k > 0)
     for (int i = 0; i < NX; ++i) {
       lb0[i] = a.lbw[ixw<NX, NU>(k, i)];
       ub0[i] = a.ubw[ixw<NX, NU>(k, i)];
@@ -293,11 +293,12 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       ub0[NX + i] = a.ubw[iuw<NX, NU>(k, i)];
     }
   int nbnd_l = 0;
+  constexpr bool kXB = XBoundsOf<Model>::value;  // false: no state is bounded (compile-time)
 #pragma unroll
   for (int i = 0; i < NZ; ++i) {
     const bool own = (i < NX) ? hasX : hasU;
-    hL[i] = own && lb0[i] > -kInfBound;
-    hU[i] = own && ub0[i] < kInfBound;
+    hL[i] = (kXB || i >= NX) && own && lb0[i] > -kInfBound;
+    hU[i] = (kXB || i >= NX) && own && ub0[i] < kInfBound;
     nbnd_l += (int)hL[i] + (int)hU[i];
   }
   // lb / ub: registers, or (kBndLds) views of this lane's LDS column re-read in every phase
@@ -810,13 +811,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
     for (int i = 0; i < NZ; ++i) {
       rd[i] += zU[i] - zL[i];
-      Ed = fmax(Ed, fabs(rd[i]));
+      Ed = qmax_abs(Ed, rd[i]);
       z1 += zL[i] + zU[i];
-      if (hL[i]) Ecomp0 = fmax(Ecomp0, fabs((z[i] - lb[i]) * zL[i]));
-      if (hU[i]) Ecomp0 = fmax(Ecomp0, fabs((ub[i] - z[i]) * zU[i]));
+      // branchless (the asm max cannot be speculated; max(E, 0) = E for E >= 0)
+      Ecomp0 = qmax_abs(Ecomp0, hL[i] ? (z[i] - lb[i]) * zL[i] : 0.0);
+      Ecomp0 = qmax_abs(Ecomp0, hU[i] ? (ub[i] - z[i]) * zU[i] : 0.0);
     }
 #pragma unroll
-    for (int i = 0; i < NX; ++i) Ec = fmax(Ec, fmax(fabs(cdef[i]), fabs(c0[i])));
+    for (int i = 0; i < NX; ++i) Ec = qmax_abs(qmax_abs(Ec, cdef[i]), c0[i]);
     Ed = gmax<G>(Ed, xw);
     Ec = gmax<G>(Ec, xw);
     Ecomp0 = gmax<G>(Ecomp0, xw);
@@ -870,8 +872,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       double Ecm = 0;
 #pragma unroll
       for (int i = 0; i < NZ; ++i) {
-        if (hL[i]) Ecm = fmax(Ecm, fabs((z[i] - lb[i]) * zL[i] - mu));
-        if (hU[i]) Ecm = fmax(Ecm, fabs((ub[i] - z[i]) * zU[i] - mu));
+        Ecm = qmax_abs(Ecm, hL[i] ? (z[i] - lb[i]) * zL[i] - mu : 0.0);
+        Ecm = qmax_abs(Ecm, hU[i] ? (ub[i] - z[i]) * zU[i] - mu : 0.0);
       }
       Ecm = gmax<G>(Ecm, xw);
       const double Emu = fmax(fmax(Ed / sd, Ec), Ecm / sc);
@@ -978,7 +980,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         }
         double dev = 0.0, mag = 1.0;
         if (hasU) {
-          okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, Aop, Bop, cdef, nx_, nx_ + NP, P, p, fac);
+          okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, false, AOneOf<Model>::value>(Hd, gp, Aop, Bop, cdef, nx_,
+                                                                                                 nx_ + NP, P, p, fac);
 #pragma unroll
           for (int i = 0; i < NP; ++i) {
             dev = fmax(dev, fabs(P[i] - e.J[i]));
@@ -1063,7 +1066,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
                 okl = okd;
               }
               else
-                okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p,
+                okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec, AOneOf<Model>::value>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p,
                                                                                      fac);
             }
           }
@@ -1094,7 +1097,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
                     okl = okd;
                   }
                   else
-                    okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p,
+                    okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec, AOneOf<Model>::value>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p,
                                                                                          fac);
                 }
               }
@@ -1321,10 +1324,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         if (dzU[i] < 0) az_l = fmin(az_l, -tau * zU[i] * rcp64(dzU[i]));
       }
       const bool own = (i < NX) ? hasX : hasU;
-      if (own) {
-        tiny_l = fmax(tiny_l, fabs(dz[i]) * rcp64(1.0 + fabs(z[i])));
-        gd_l += gp[i] * dz[i];
-      }
+      tiny_l = qmax_abs(tiny_l, own ? dz[i] * rcp64(1.0 + fabs(z[i])) : 0.0);
+      if (own) gd_l += gp[i] * dz[i];
     }
     const double amax = gmin<G>(amax_l, xw), tiny = gmax<G>(tiny_l, xw);
     double az = gmin<G>(az_l, xw);  // dual step length (a second-order correction replaces it)
@@ -1368,7 +1369,13 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           double lt[NX];
 #pragma unroll
           for (int i = 0; i < NX; ++i) lt[i] = fma(alpha, dlam[i], lam[i]);
+#ifdef MPCX_STAMP_EVAL
+          STAMP(9);  // diagnostic: the trial's evaluation accumulates into phase 9
+#endif
           eval_at(zt, lt);
+#ifdef MPCX_STAMP_EVAL
+          STAMP(6);
+#endif
           fresh = false;  // until accepted
 #pragma unroll
           for (int i = 0; i < NX; ++i) tht_l += fabs(cdef[i]) + fabs(c0[i]);

@@ -40,6 +40,7 @@ struct UnicycleModel {
   static constexpr int NX = 3, NU = 2;
   static constexpr unsigned long long AMASK = (1ull << 0) | (1ull << 2) | (1ull << 4) | (1ull << 5) | (1ull << 8);
   static constexpr unsigned long long BMASK = (1ull << 0) | (1ull << 1) | (1ull << 2) | (1ull << 3) | (1ull << 5);
+  static constexpr unsigned long long AONE = (1ull << 0) | (1ull << 4) | (1ull << 8);  // A's unit diagonal
   // the line search's first trial evaluates derivatives, not just values: accepted (the
   // usual case) it is the next iteration's evaluation, which is then skipped
   static constexpr bool kEvalInSearch = true;
@@ -86,6 +87,13 @@ struct UnicycleModel {
     const double u2[2] = {z[3], z[4]};
     uni_value(a.sp, z, u2, c.xr, c.ur, xf, q);
   }
+};
+
+// The same model for problems without state bounds (configs 1 and 2: X free, |v| <= 1,
+// |w| <= pi/4): the launch picks it when no node has a finite state bound, and every state-bound
+// term folds away at compile time (kernels.h kXB).
+struct UnicycleFreeModel : UnicycleModel {
+  static constexpr bool kXBounds = false;
 };
 
 // The same model with the backward Riccati recursion as a log-depth scan (pscan.h).  The scan's

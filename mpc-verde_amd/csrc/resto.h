@@ -176,7 +176,7 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const
     lb[i] = -1e20;
     ub[i] = 1e20;
   }
-  if (hasX && k > 0)
+  if (XBoundsOf<Model>::value && hasX && k > 0)
     for (int i = 0; i < NX; ++i) {
       lb[i] = lbw[k == 0 ? i : NX + NZ * (k - 1) + NU + i];
       ub[i] = ubw[k == 0 ? i : NX + NZ * (k - 1) + NU + i];
@@ -188,8 +188,8 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const
     }
 #pragma unroll
   for (int i = 0; i < NZ; ++i) {
-    hL[i] = own(i) && lb[i] > -kInfBound;
-    hU[i] = own(i) && ub[i] < kInfBound;
+    hL[i] = (XBoundsOf<Model>::value || i >= NX) && own(i) && lb[i] > -kInfBound;
+    hU[i] = (XBoundsOf<Model>::value || i >= NX) && own(i) && ub[i] < kInfBound;
   }
 
   // ---- the iterate and its Newton step (RestoWs)
@@ -644,7 +644,8 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const
       bool okl = true;
       auto step = [&](double* Pin_, double* pin_) __attribute__((always_inline)) {
         const bool okt = resto_transform<NX>(D1, Pin_, pin_);
-        okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK>(Hd, gp, A, Bm, ct1, Pin_, pin_, P, p, fac) && okt;
+        okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, false, AOneOf<Model>::value>(Hd, gp, A, Bm, ct1, Pin_,
+                                                                                                    pin_, P, p, fac) && okt;
       };
       if constexpr (G <= 64) {
         for (int j = N - 1; j >= 0; --j) {

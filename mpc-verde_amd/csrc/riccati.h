@@ -11,6 +11,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "collectives.h"
 
 namespace mpcx {
@@ -46,12 +48,59 @@ struct Fac {  // LDL^T data of Huu' kept for the gains (per lane)
 // SREORD: s = (P_{k+1} c) + p_{k+1} with the product summed first -- the order in which the
 // DEC step takes it precomputed off the chain (vpre = P_{k+1} c, riccati_pc), so the two
 // variants of a model that uses DEC give the same bits.
-template <int NX, int NU, unsigned long long AMASK, unsigned long long BMASK, bool DEC = false, bool SREORD = false>
+// Model::AONE (structural unit entries of A, riccati_step) if the model declares it, else 0
+template <class M, class = void>
+struct AOneOf {
+  static constexpr unsigned long long value = 0;
+};
+template <class M>
+struct AOneOf<M, std::void_t<decltype(M::AONE)>> {
+  static constexpr unsigned long long value = M::AONE;
+};
+
+// Model::kXBounds if the model declares it, else true: false = the model's solve kernel never
+// sees finite state bounds (the launch picks it only then), so every state-bound term of the
+// barrier, the complementarity, the fraction to the boundary and the bound-dual update is a
+// compile-time zero
+template <class M, class = void>
+struct XBoundsOf {
+  static constexpr bool value = true;
+};
+template <class M>
+struct XBoundsOf<M, std::void_t<decltype(M::kXBounds)>> {
+  static constexpr bool value = M::kXBounds;
+};
+
+// AONE: bit r*NX+j set = A[r][j] is exactly 1 (a model's structural unit entries, within AMASK):
+// such terms enter as additions, and the sums start from them.  Hux' is formed as A^T (P B) when
+// A's columns are sparser than B's (the unicycle: A = I + two entries in column 2), else as
+// B^T (P A).
+__host__ __device__ constexpr int popc64(unsigned long long v) { return v ? (int)(v & 1ull) + popc64(v >> 1) : 0; }
+template <int NX, int NU>
+__host__ __device__ constexpr unsigned long long col_mask(unsigned long long mask, int ncol, int j, int nrow) {
+  unsigned long long r = 0;
+  for (int m = 0; m < nrow; ++m) r |= ((mask >> (m * ncol + j)) & 1ull) << m;
+  return r;
+}
+template <int NX, int NU, unsigned long long AMASK, unsigned long long BMASK>
+__host__ __device__ constexpr bool hux_by_atpb() {
+  int bt = 0, at = 0;
+  for (int l = 0; l < NU; ++l)
+    for (int j = 0; j < NX; ++j) {
+      bt += popc64(col_mask<NX, NU>(BMASK, NU, l, NX));
+      at += popc64(col_mask<NX, NU>(AMASK, NX, j, NX));
+    }
+  return at < bt;
+}
+
+template <int NX, int NU, unsigned long long AMASK, unsigned long long BMASK, bool DEC = false, bool SREORD = false,
+          unsigned long long AONE = 0>
 __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp, const double* A, const double* Bm,
                                              const double* c, const double* P, const double* p, double* Pn,
                                              double* pn, Fac<NX, NU>& f, const double* Pown = nullptr,
                                              const double* vpre = nullptr) {
   static_assert(!DEC || SREORD, "DEC takes s in the SREORD order");
+  static_assert((AONE & ~AMASK) == 0, "unit entries must be inside AMASK");
   constexpr int NZ = NX + NU;
   static_assert(NU == 1 || NU == 2, "NU must be 1 or 2");
   auto Pm = [&](int i, int j) { return P[symix(i, j, NX)]; };
@@ -76,8 +125,14 @@ __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp,
       double acc = 0.0;
       bool first = true;
 #pragma unroll
+      for (int m = 0; m < NX; ++m)  // unit terms first (additions), then the others as FMAs
+        if (AONE & (1ull << (m * NX + j))) {
+          acc = first ? Pm(r, m) : acc + Pm(r, m);
+          first = false;
+        }
+#pragma unroll
       for (int m = 0; m < NX; ++m)
-        if (AMASK & (1ull << (m * NX + j))) {
+        if ((AMASK & ~AONE) & (1ull << (m * NX + j))) {
           acc = first ? Pm(r, m) * A[m * NX + j] : fma(Pm(r, m), A[m * NX + j], acc);
           first = false;
         }
@@ -106,14 +161,24 @@ __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp,
         if (AMASK & (1ull << (m * NX + i))) acc = fma(A[m * NX + i], PA[m * NX + j], acc);
       Hxx[i * NX + j] = acc;
     }
+  constexpr bool kAtPB = hux_by_atpb<NX, NU, AMASK, BMASK>();
 #pragma unroll
   for (int l = 0; l < NU; ++l) {
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       double acc = Hd[symix(j, NX + l, NZ)];
+      if constexpr (kAtPB) {  // Hux'[l][j] = Hd + sum_m A[m][j] (P B)[m][l]
 #pragma unroll
-      for (int m = 0; m < NX; ++m)
-        if (BMASK & (1ull << (m * NU + l))) acc = fma(Bm[m * NU + l], PA[m * NX + j], acc);
+        for (int m = 0; m < NX; ++m)
+          if (AONE & (1ull << (m * NX + j))) acc += PB[m * NU + l];
+#pragma unroll
+        for (int m = 0; m < NX; ++m)
+          if ((AMASK & ~AONE) & (1ull << (m * NX + j))) acc = fma(A[m * NX + j], PB[m * NU + l], acc);
+      } else {  // Hd + sum_m B[m][l] (P A)[m][j]
+#pragma unroll
+        for (int m = 0; m < NX; ++m)
+          if (BMASK & (1ull << (m * NU + l))) acc = fma(Bm[m * NU + l], PA[m * NX + j], acc);
+      }
       Hux[l * NX + j] = acc;
     }
 #pragma unroll

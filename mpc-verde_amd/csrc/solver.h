@@ -40,6 +40,7 @@ struct SolveArgs {
   double acc_tol, acc_dual_inf_tol, acc_constr_viol_tol, acc_compl_inf_tol, acc_obj_change_tol;
   int acc_iter;         // <= 0: no acceptable-level termination
   int restoration;      // soft restoration + restoration phase on a failed line search (models with kResto)
+  int xbnd;             // 1: some node has a finite state bound in lbw/ubw (picks the kernel variant)
   double* ws;           // restoration workspace: slot i of thread t at ws[i * ws_stride + t] (kResto models)
   long ws_stride;
   // park flag (after the workspace): the solve launch stores park_epoch there when it parks an

@@ -105,6 +105,7 @@ int resto_ws_slots(int model, int nx, int nu) {
   int diag_set_stamps_##tag(void*);                                                                             \
   int diag_set_counters_##tag(void*);
 MPCX_DECLARE(unicycle)
+MPCX_DECLARE(unicycle_xfree)
 MPCX_DECLARE(unicycle_scan)
 MPCX_DECLARE(linear4)
 MPCX_DECLARE(linear5)
@@ -130,7 +131,8 @@ static int unicycle_scan_min_n() {
 #define MPCX_DISPATCH(a, FN, ...)                                                 \
   do {                                                                            \
     if ((a).model == 1)                                                           \
-      return (a).N >= unicycle_scan_min_n() ? FN##_unicycle_scan(__VA_ARGS__) : FN##_unicycle(__VA_ARGS__); \
+      return (a).N >= unicycle_scan_min_n() ? FN##_unicycle_scan(__VA_ARGS__)                              \
+             : (a).xbnd ? FN##_unicycle(__VA_ARGS__) : FN##_unicycle_xfree(__VA_ARGS__);                       \
     if ((a).model == 2 && (a).nx == 4 && (a).nu == 1) return FN##_linear4(__VA_ARGS__); \
     if ((a).model == 2 && (a).nx == 5 && (a).nu == 1) return FN##_linear5(__VA_ARGS__); \
     if ((a).model == 2 && (a).nx == 4 && (a).nu == 2) return FN##_linear4x2(__VA_ARGS__); \
@@ -159,12 +161,12 @@ hipError_t launch_shift(const SolveArgs& a, double* P, const double* W, double* 
 // diagnostic build: every model unit holds its own copy of the buffer pointers
 extern "C" int mpcx_diag_set_stamp_buffer(void* d_buf) {
   using namespace mpcx;
-  return diag_set_stamps_unicycle(d_buf) | diag_set_stamps_unicycle_scan(d_buf) | diag_set_stamps_linear4(d_buf) | diag_set_stamps_linear5(d_buf) | diag_set_stamps_linear4x2(d_buf) |
+  return diag_set_stamps_unicycle(d_buf) | diag_set_stamps_unicycle_xfree(d_buf) | diag_set_stamps_unicycle_scan(d_buf) | diag_set_stamps_linear4(d_buf) | diag_set_stamps_linear5(d_buf) | diag_set_stamps_linear4x2(d_buf) |
          diag_set_stamps_kin_bicycle(d_buf) | diag_set_stamps_dyn_bicycle(d_buf) | diag_set_stamps_cartpole(d_buf);
 }
 extern "C" int mpcx_diag_set_counter_buffer(void* d_buf) {
   using namespace mpcx;
-  return diag_set_counters_unicycle(d_buf) | diag_set_counters_unicycle_scan(d_buf) | diag_set_counters_linear4(d_buf) | diag_set_counters_linear5(d_buf) | diag_set_counters_linear4x2(d_buf) |
+  return diag_set_counters_unicycle(d_buf) | diag_set_counters_unicycle_xfree(d_buf) | diag_set_counters_unicycle_scan(d_buf) | diag_set_counters_linear4(d_buf) | diag_set_counters_linear5(d_buf) | diag_set_counters_linear4x2(d_buf) |
          diag_set_counters_kin_bicycle(d_buf) | diag_set_counters_dyn_bicycle(d_buf) | diag_set_counters_cartpole(d_buf);
 }
 #endif
