@@ -1051,6 +1051,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           }
         }
         if constexpr (G <= 64) {
+          // the chain: one step per node, lane j only.  Models without the decoupled suffix take
+          // the inertia verdict of their step from its factors after the chain, on all lanes at
+          // once (fac_ok), so no lane-mask merge sits on the chain
+#pragma unroll 2
           for (int j = N - 1; j >= 0; --j) {
             const bool cheap = reuse && j >= kb;
             double Pin_[NP], pin_[NX];
@@ -1061,15 +1065,22 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
             for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
             if (seq && k == j) {
-              if (cheap) {  // group-uniform
-                dec_vector_step<NX, NU, Model::AMASK, Model::BMASK>(gp, Aop, Bop, vpc, pin_, p, fac);
-                okl = okd;
+              if constexpr (kDec) {
+                if (cheap) {  // group-uniform
+                  dec_vector_step<NX, NU, Model::AMASK, Model::BMASK>(gp, Aop, Bop, vpc, pin_, p, fac);
+                  okl = okd;
+                } else {
+                  okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec, AOneOf<Model>::value>(
+                      Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p, fac);
+                }
+              } else {
+                (void)riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec, AOneOf<Model>::value>(
+                    Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p, fac);
               }
-              else
-                okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec, AOneOf<Model>::value>(Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p,
-                                                                                     fac);
             }
           }
+          if constexpr (!kDec)
+            if (seq) okl = !hasU || fac_ok<NX, NU>(fac);
         } else {  // wave by wave, N-side first; the value function crosses waves through LDS
           const int wv = (int)(threadIdx.x >> 6);
           for (int ph = XWave<G>::W - 1; ph >= 0; --ph) {

@@ -327,6 +327,17 @@ __device__ __forceinline__ void dec_vector_step(const double* gp, const double* 
   if constexpr (NU == 2) f.g1 = fma(-f.t, gp[NX], gp[NX + 1]);
 }
 
+// The inertia verdict of a step from its factors (off the chain, all lanes at once): Huu' is
+// positive definite iff its LDL^T pivots are -- r0 = 1/d0 and (NU = 2) r1 = d0/det positive and
+// finite.  The same answer as the step's own test (d0 > 0, det > 0) but where a reciprocal
+// overflows (a pivot below ~1e-308) or is NaN, which the test reads as indefinite too.
+template <int NX, int NU>
+__device__ __forceinline__ bool fac_ok(const Fac<NX, NU>& f) {
+  const bool a = f.r0 > 0.0 && f.r0 < INFINITY;
+  if constexpr (NU == 1) return a;
+  return a && f.r1 > 0.0 && f.r1 < INFINITY;
+}
+
 // K = -Huu'^{-1} Hux', kf = -Huu'^{-1} gu' from the LDL^T data (off the critical path).
 template <int NX, int NU>
 __device__ __forceinline__ void riccati_gains(const Fac<NX, NU>& f, double* K, double* kf) {

@@ -27,7 +27,8 @@ def build():
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "libipm_ref.so")
+        # ORACLE_LIB: another build of the same oracle (the sanitizer build, tests/test_asan.py)
+        path = os.environ.get("ORACLE_LIB") or os.path.join(_HERE, "libipm_ref.so")
         if not os.path.exists(path):
             build()
         _LIB = ctypes.CDLL(path)

@@ -87,3 +87,66 @@ def test_moment_assembly_equals_per_point_formula_and_oracle(harness, cost, M):
     mom1 = blocks(run(harness, n, T, M, cost, Q, R, X, U, XR, UR, np.zeros_like(L), 1.0)[0])
     np.testing.assert_allclose(mom2["g"], 0.25 * mom1["g"], rtol=1e-13, atol=1e-13)
     np.testing.assert_allclose(mom2["H"], 0.25 * mom1["H"], rtol=1e-13, atol=1e-13)
+
+
+def pack(M):
+    n = M.shape[-1]
+    return np.stack([M[..., i, j] for i in range(n) for j in range(i, n)], axis=-1)
+
+
+def unpack(v, n):
+    M = np.zeros(v.shape[:-1] + (n, n))
+    t = 0
+    for i in range(n):
+        for j in range(i, n):
+            M[..., i, j] = M[..., j, i] = v[..., t]
+            t += 1
+    return M
+
+
+def test_riccati_step_vs_dense_formula(harness):
+    """One backward step of the config-2 chain (riccati.h riccati_step with the unicycle's masks,
+    unit entries and Hux' = A^T (P B)) against the dense formulas: H' = Hd + M^T P M, g' = gp +
+    M^T (P c + p) with M = [A B]; P_k = Hxx' - Hux'^T Huu'^-1 Hux', p_k = gx' - Hux'^T Huu'^-1
+    gu', K = -Huu'^-1 Hux', k_f = -Huu'^-1 gu' (<= 1e-10 relative), and the inertia verdict taken
+    from the factors after the chain (fac_ok) equals the step's own test and numpy's."""
+    import torch
+
+    rng = np.random.default_rng(3)
+    n = 8192
+    T = 0.2
+    A = np.tile(np.eye(3), (n, 1, 1))
+    A[:, 0, 2], A[:, 1, 2] = rng.normal(size=n), rng.normal(size=n)
+    Bm = np.zeros((n, 3, 2))
+    Bm[:, 0:2, :] = rng.normal(size=(n, 2, 2)) * 0.2
+    Bm[:, 2, 1] = T
+    L = rng.normal(size=(n, 5, 5))
+    Hd = np.einsum("bij,bkj->bik", L, L) * 0.5
+    Hd[n // 2:] -= 1.5 * np.eye(5)  # half of them indefinite in places
+    Lp = rng.normal(size=(n, 3, 3))
+    P1 = np.einsum("bij,bkj->bik", Lp, Lp)
+    gp, c, p1 = rng.normal(size=(n, 5)), rng.normal(size=(n, 3)) * 0.1, rng.normal(size=(n, 3))
+    inp = np.concatenate([pack(Hd), gp, A.reshape(n, 9), Bm.reshape(n, 6), c, pack(P1), p1], axis=1)
+    d_in = torch.from_numpy(np.ascontiguousarray(inp)).cuda()
+    d_out = torch.zeros(n * 18, dtype=torch.float64, device="cuda")
+    harness.riccati_check.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    assert harness.riccati_check(n, ctypes.c_void_p(d_in.data_ptr()), ctypes.c_void_p(d_out.data_ptr())) == 0
+    o = d_out.cpu().numpy().reshape(n, 18)
+    M = np.concatenate([A, Bm], axis=2)
+    H = Hd + np.einsum("bki,bkl,blj->bij", M, P1, M)
+    g = gp + np.einsum("bki,bk->bi", M, np.einsum("bij,bj->bi", P1, c) + p1)
+    Huu, Hux, gu = H[:, 3:, 3:], H[:, 3:, :3], g[:, 3:]
+    pd = np.all(np.linalg.eigvalsh(Huu) > 0, axis=1)
+    assert 0.2 * n < pd.sum() < 0.95 * n
+    assert not np.any(o[:, 9] == 0.5)  # fac_ok == the step's own test on every instance
+    np.testing.assert_array_equal(o[:, 9] == 1.0, pd)
+    iH = np.linalg.inv(Huu[pd])
+    K = -iH @ Hux[pd]
+    kf = -np.einsum("bij,bj->bi", iH, gu[pd])
+    Pn = H[pd, :3, :3] + np.einsum("bki,bkj->bij", Hux[pd], K)
+    pn = g[pd, :3] + np.einsum("bki,bk->bi", Hux[pd], kf)
+    for got, ref in ((o[pd, 0:6], pack(Pn)), (o[pd, 6:9], pn), (o[pd, 10:16], K.reshape(-1, 6)), (o[pd, 16:18], kf)):
+        scale = np.maximum(np.max(np.abs(ref), axis=1, keepdims=True), 1.0)
+        cond = np.linalg.cond(Huu[pd])[:, None]
+        err = np.abs(got - ref) / scale / np.maximum(cond, 1.0)
+        assert err.max() <= 1e-12, err.max()
