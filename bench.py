@@ -97,6 +97,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--group-policy", type=int, default=0, choices=(0, 1),
+                    help="mpcx_spec.group_policy: 0 widens lane groups to fill the SIMDs, 1 keeps the smallest")
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5),
                     help="2: point-to-point N=20 B=1024 (headline); 3: circular tracking N=30 B=4096; "
                          "4: LTV lateral lane change N=50 B=1024/GPU; 5: cart-pole QP N=100 B=2048/GPU")
@@ -389,7 +391,7 @@ def main():
     # others run IPOPT's defaults (mpctools / no reference script)
     ipopt = ({"max_iter": 2000, "acceptable_tol": 1e-8, "acceptable_obj_change_tol": 1e-6}
              if cfg == 2 and variant is None else {"max_iter": 3000})
-    solver = mpcx.nlpsol("bench", "mi355x", ocp, {"ipopt": ipopt}, device=local)
+    solver = mpcx.nlpsol("bench", "mi355x", ocp, {"ipopt": ipopt, "group_policy": args.group_policy}, device=local)
     stream = torch.cuda.current_stream()
 
     if args.profile_sweep_only:

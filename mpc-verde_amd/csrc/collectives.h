@@ -140,6 +140,21 @@ __device__ __forceinline__ double gmin(double v, XWave<G>& xw) {
 __device__ __forceinline__ double from_next(double v) { return dpp<kWaveShl1>(v); }
 __device__ __forceinline__ double from_prev(double v) { return dpp<kWaveShr1>(v); }
 
+// Partner of level d (1, 2, 4, 8, 16, 32) of a wave-wide inclusive prefix scan, as DPP moves
+// (VALU, no LDS crossbar round trip): row_shr:d inside each 16-lane row for d <= 8, then
+// row_bcast:15 (lane 16r-1 to row r) and row_bcast:31 (lane 31 to rows 2, 3).  After the
+// in-row levels lane l holds the row's prefix up to l; the broadcasts carry the previous
+// rows' total in.  scan_takes<d>(kw) says whether the lane at wave position kw combines.
+template <int D>
+__device__ __forceinline__ double scan_partner(double v) {
+  static_assert(D == 1 || D == 2 || D == 4 || D == 8 || D == 16 || D == 32, "scan level");
+  return dpp<D <= 8 ? 0x110 + D : D == 16 ? 0x142 : 0x143>(v);
+}
+template <int D>
+__device__ __forceinline__ bool scan_takes(int kw) {
+  return D <= 8 ? (kw & 15) >= D : (kw & D) != 0;
+}
+
 // value of lane `src` of the wave (any lane; ds_bpermute through the LDS crossbar, no LDS memory)
 __device__ __forceinline__ double from_lane(double v, int src) {
   const long long b = __double_as_longlong(v);

@@ -824,9 +824,24 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     Ecomp0 = gmax<G>(Ecomp0, xw);
     lam1 = gsum<G>(lam1, xw);
     z1 = gsum<G>(z1, xw);
-    const double sd = fmax(kSmax, (lam1 + z1) / (double)(ng + nw)) / kSmax;
-    const double sc = fmax(kSmax, nbound > 0 ? z1 / nbound : 0.0) / kSmax;
-    const double E0 = fmax(fmax(Ed / sd, Ec), Ecomp0 / sc);
+    // IPOPT's scalings s_d = max(s_max, (|lam|_1 + |z|_1) / (m + n)) / s_max and s_c = max(s_max,
+    // |z|_1 / n_b) / s_max are exactly 1 unless the sum exceeds s_max times the count (a rounded
+    // quotient that reaches s_max from above still gives 1): the IEEE divisions -- two group-
+    // uniform ~12-instruction sequences each -- only run on waves where some instance needs them
+    const bool sd1 = !(lam1 + z1 > kSmax * (double)(ng + nw));
+    const bool sc1 = !(nbound > 0 && z1 > kSmax * nbound);
+    double sd = 1.0, sc = 1.0, Eds = Ed, Ecs = Ecomp0;  // Ed / s_d, Ecomp0 / s_c
+    if (__any(!sd1 || !sc1)) {
+      if (!sd1) {
+        sd = fmax(kSmax, (lam1 + z1) / (double)(ng + nw)) / kSmax;
+        Eds = Ed / sd;
+      }
+      if (!sc1) {
+        sc = fmax(kSmax, z1 / nbound) / kSmax;
+        Ecs = Ecomp0 / sc;
+      }
+    }
+    const double E0 = fmax(fmax(Eds, Ec), Ecs);
     // IPOPT OptimalityErrorConvergenceCheck: tol with the unscaled dual infeasibility,
     // constraint violation and complementarity tests; then the acceptable level (all of
     // acceptable_* and the objective change from the previous iterate) for acceptable_iter
@@ -876,7 +891,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         Ecm = qmax_abs(Ecm, hU[i] ? (ub[i] - z[i]) * zU[i] - mu : 0.0);
       }
       Ecm = gmax<G>(Ecm, xw);
-      const double Emu = fmax(fmax(Ed / sd, Ec), Ecm / sc);
+      double Ecms = Ecm;  // Ecm / s_c
+      if (__any(!sc1))
+        if (!sc1) Ecms = Ecm / sc;
+      const double Emu = fmax(fmax(Eds, Ec), Ecms);
       const bool dec = !done && (Emu <= kKappaEps * mu || (tiny_flag && rep == 0)) && mu > mu_min;
       if (dec && !done) DIAG(3);
       if (dec) {
@@ -1199,9 +1217,12 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       }
       {
         // dx_k = T_{k-1}( ... T_0(c0)) with affine T_j(x) = Acl_j x + ccl_j: an inclusive
-        // parallel prefix of map compositions (Hillis-Steele, log2 64 levels per wave, all
-        // lanes busy) instead of N+1 dependent steps.  Lane k starts with T_{k-1} (lane 0:
-        // the constant map c0) and composes with the partial map of lane k-d at each level.
+        // parallel prefix of map compositions (log2 GW levels per wave, all lanes busy) instead
+        // of N+1 dependent steps.  Lane k starts with T_{k-1} (lane 0: the constant map c0) and
+        // composes with the partial map of its DPP partner at each level: Kogge-Stone inside
+        // each 16-lane row, then the previous rows' totals by row broadcasts (scan_partner; the
+        // ds_bpermute version of the same scan, Hillis-Steele over lane k-d: config 2 16.3 us per
+        // IPM iteration against 15.8 us with the DPP partners, config 3 35.0 against 33.7 us).
         // Multi-wave groups scan every wave at once; the first lane of wave w gets
         // T_{64w-1} from wave w-1 through LDS, and the waves' partial results are chained
         // by one LDS handoff of dx per wave boundary.
@@ -1233,15 +1254,16 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           for (int i = 0; i < NX; ++i) cm[i] = (k == 0) ? c0v_[i] : prv[NX * NX + i];
         }
         const int kw = k & (GW - 1);  // position inside the wave
-#pragma unroll
-        for (int d = 1; d < GW; d <<= 1) {
-          const int src = (lane - d) & 63;
+        // one level: compose with the partial map of the DPP partner (collectives.h scan_partner)
+        auto level = [&](auto dc) __attribute__((always_inline)) {
+          constexpr int d = decltype(dc)::value;
+          if constexpr (d < GW) {
           double Ao[NX * NX], co[NX];
 #pragma unroll
-          for (int i = 0; i < NX * NX; ++i) Ao[i] = from_lane(Am[i], src);
+          for (int i = 0; i < NX * NX; ++i) Ao[i] = scan_partner<d>(Am[i]);
 #pragma unroll
-          for (int i = 0; i < NX; ++i) co[i] = from_lane(cm[i], src);
-          if (kw >= d) {  // compose: (Am, cm) o (Ao, co)
+          for (int i = 0; i < NX; ++i) co[i] = scan_partner<d>(cm[i]);
+          if (scan_takes<d>(kw)) {  // compose: (Am, cm) o (Ao, co)
             double An[NX * NX], cn[NX];
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -1262,7 +1284,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
             for (int i = 0; i < NX; ++i) cm[i] = cn[i];
           }
-        }
+          }
+        };
+        level(std::integral_constant<int, 1>{});
+        level(std::integral_constant<int, 2>{});
+        level(std::integral_constant<int, 4>{});
+        level(std::integral_constant<int, 8>{});
+        level(std::integral_constant<int, 16>{});
+        level(std::integral_constant<int, 32>{});
         if constexpr (G > 64) {
           // wave w's lanes hold maps dx_{64w-1} -> dx_k; chain the waves in order
           for (int ph = 1; ph < XWave<G>::W; ++ph) {
@@ -1317,7 +1346,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     STAMP(5);
     phase();
     // ------------------------------------------------------------ bound-dual step, fraction to boundary
-    double amax_l = 1.0, az_l = 1.0, tiny_l = 0.0, gd_l = 0.0;
+    double amax_l = 1.0, az_l = 1.0, tiny_l = -1.0, gd_l = 0.0;
 #pragma unroll
     for (int i = 0; i < NZ; ++i) {
       dzL[i] = dzU[i] = 0.0;
@@ -1335,13 +1364,16 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         if (dzU[i] < 0) az_l = fmin(az_l, -tau * zU[i] * rcp64(dzU[i]));
       }
       const bool own = (i < NX) ? hasX : hasU;
-      tiny_l = qmax_abs(tiny_l, own ? dz[i] * rcp64(1.0 + fabs(z[i])) : 0.0);
+      // IPOPT's tiny step test max |dz_i| / (1 + |z_i|) < 10 eps as the sign of
+      // |dz_i| - 10 eps (1 + |z_i|) (one fma, no reciprocal)
+      tiny_l = qmax(tiny_l, own ? fma(-10.0 * kEps, 1.0 + fabs(z[i]), fabs(dz[i])) : -1.0);
       if (own) gd_l += gp[i] * dz[i];
     }
     const double amax = gmin<G>(amax_l, xw), tiny = gmax<G>(tiny_l, xw);
     double az = gmin<G>(az_l, xw);  // dual step length (a second-order correction replaces it)
+    const bool tinystep = tiny < 0.0;
     if (!done && amax < 1.0) DIAG(4);
-    if (!done && tiny < 10.0 * kEps) DIAG(5);
+    if (!done && tinystep) DIAG(5);
     const double gd = gsum<G>(gd_l, xw);
 
     STAMP(6);
@@ -1351,7 +1383,6 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
     for (int i = 0; i < NX; ++i) thk_l += fabs(cdef[i]) + fabs(c0[i]);
     const double thk = gsum<G>(thk_l, xw), phk = gsum<G>(phk_l, xw);
-    const bool tinystep = tiny < 10.0 * kEps;
     double alpha = amax;
     bool searching = !done && !tinystep && !(kRes && soft);
     bool accepted = !done && tinystep;
