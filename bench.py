@@ -43,7 +43,7 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # FP64 vector (VALU) peak: AMD's MI355X spec, half the FP32 vector peak of 157.3 TF/s
 # (MI355X_MICROARCH.md); the solve kernel issues scalar-per-lane FP64 FMAs, no MFMA
 PEAK_FP64_TFLOPS = 78.6
-SOLVE_PMC = os.path.join("profiles", "r02_solve_kernel_pmc.json")
+SOLVE_PMC = os.path.join("profiles", "r03_solve_kernel_pmc.json")
 SWEEP_BYTES_PER_STAGE = 256  # read x_k,u_k,x_{k+1} (64 B) + write c,q,A,B,grad q (192 B)
 SWEEP_BYTES_PER_INSTANCE = 48  # P
 
@@ -207,7 +207,7 @@ def _cold(P, N, nlp_ref):
     return nlp_ref.join_w(X, np.zeros((P.shape[0], N, 2)))
 
 
-CFG_KERNEL = {2: "UnicycleModel", 3: "UnicycleModel", 4: "LinearModel<4, 1>", 5: "LinearModel<5, 1>"}
+CFG_KERNEL = {2: "UnicycleFreeModel", 3: "UnicycleScanModel", 4: "LinearModel<4, 1>", 5: "LinearModel<5, 1>"}
 VARIANT_KERNEL = {"kin_bicycle": "KinBicycle", "dyn_bicycle": "DynBicycle", "cartpole": "CartPole"}
 
 
@@ -234,29 +234,110 @@ def usable_cpus():
     return max(1, n)
 
 
-def solve_roofline(kernel_substr, G, n_nodes, group_iters, ms):
-    """Roofline entry of the fused solve kernel from the committed PMC characterisation."""
+# ---- algorithmic FP64 work of one IPM iteration of one instance
+# Per node with an interval: one stage evaluation E (Model::derivs) + one backward Riccati
+# step R (riccati_step + riccati_gains), both measured per unit on the device by
+# tools/flop_probe.py (profiles/r03_flop_probe.json), + the IPM's vector work V below, counted
+# from the sequential algorithm (the log-depth scans' extra compositions, group-uniform
+# recomputation on every lane, padding lanes and the line search's further trials are not
+# algorithmic work and are not counted).  Linear models' E is counted analytically (their
+# Jacobians and Hessians are tables).
+FLOP_PROBE = os.path.join("profiles", "r03_flop_probe.json")
+ALGO_KEYS = {  # workload -> (eval key or None for a linear model, riccati key)
+    2: ("unicycle_quadrature_M4", "unicycle"), 3: ("unicycle_node_M1", "unicycle"),
+    4: (None, "linear4x1"), 5: (None, "linear5x1"),
+    "kin_bicycle": ("kin_bicycle_M1", "kin_bicycle"), "dyn_bicycle": ("dyn_bicycle_M4", "dyn_bicycle"),
+    "cartpole": ("cartpole_M1", "cartpole"),
+}
+
+
+def ipm_vector_flops(n, m, nbs):
+    """FP64 flops per node of the IPM's vector phases (n states, m inputs, nbs finite bound
+    sides), one term per phase of kernels.h's solve loop (DESIGN.md §6 lists them)."""
+    nz = n + m
+    err = n + 2 * n * n + 2 * n * m + 5 * nz + 3 * n + 2 * nbs + 5  # rd = grad L, |.|_inf, complementarity, sums
+    mu = 3 * nbs                                                    # barrier-test complementarity
+    sig = 6 * nbs + 2 * nz                                          # Sigma, barrier gradient, Hd = H + Sigma
+    fwd = 2 * m * n + 2 * n * n + 2 * n * m + n + 2 * n * n + 2 * n  # du = kf + K dx, dx+, dlam = P dx + p - lam
+    frac = 14 * nbs + 5 * nz                                        # bound-dual steps, fraction to boundary, tiny, gd
+    ls = 2 * nz + 2 * n + 3 * n + 2 * nbs + 4                       # one trial: z + a dz, lam, theta, phi
+    upd = 2 * nz + 2 * n + 8 * nbs                                  # update + kappa_sigma safeguard
+    return err + mu + sig + fwd + frac + ls + upd
+
+
+def linear_eval_flops(n, m):
+    """Linear-quadratic stage: c = A x + B u + c0 - x+, grad q = W z + w, q."""
+    nz = n + m
+    return 2 * n * nz + 2 * n + 2 * nz * nz + 4 * nz
+
+
+def algorithmic_flops_per_iteration(key, ocp, N):
+    """Algorithmic FP64 flops of one IPM iteration of one instance, or (None, reason)."""
+    path = os.path.join(ROOT, FLOP_PROBE)
+    if not os.path.exists(path):
+        return None, f"{FLOP_PROBE} missing"
+    with open(path) as f:
+        probe = json.load(f)
+    ek, rk = ALGO_KEYS[key]
+    n, m = ocp.nx, ocp.nu
+    fin = lambda v: sum(1 for x in v if np.isfinite(x))  # noqa: E731
+    nbs = fin(ocp.x_lb) + fin(ocp.x_ub) + fin(ocp.u_lb) + fin(ocp.u_ub)
+    E = linear_eval_flops(n, m) if ek is None else probe["eval"][ek]["flops_per_unit"]
+    R = probe["riccati"][rk]["flops_per_unit"]
+    V = ipm_vector_flops(n, m, nbs)
+    total = N * (E + R + V) + ipm_vector_flops(n, 0, fin(ocp.x_lb) + fin(ocp.x_ub))  # + the terminal node
+    return {"per_iteration": total, "per_node": {"eval": E, "riccati": R, "ipm_vector": V},
+            "eval_source": "analytic (table model)" if ek is None else f"{FLOP_PROBE}: eval {ek}",
+            "riccati_source": f"{FLOP_PROBE}: riccati {rk}", "bound_sides_per_node": nbs}, None
+
+
+def load_solve_pmc(kernel_substr, G):
+    """The solve kernel's record in the committed PMC characterisation, if it was measured on
+    the library built from the sources in this tree (else (None, reason): a stale record is
+    never used)."""
+    from mpcx import _lib
+
     path = os.path.join(ROOT, SOLVE_PMC)
-    if not os.path.exists(path) or ms <= 0 or group_iters <= 0:
-        return None
+    if not os.path.exists(path):
+        return None, f"{SOLVE_PMC} missing"
     with open(path) as f:
         d = json.load(f)
+    have, want = d.get("_meta", {}).get("mpcx_source_hash"), _lib.source_hash()
+    if have is None or have != want:
+        return None, f"stale: {SOLVE_PMC} measured on sources {have}, this tree is {want}"
     for k, v in d.items():
         if kernel_substr in k and f", {G}, false>" in k and v.get("f64_lane_flops_per_group_iteration"):
-            frac_lanes = min(n_nodes, G) / G
-            fl = v["f64_lane_flops_per_group_iteration"] * frac_lanes * group_iters
-            ach = fl / (ms * 1e-3) / 1e12
-            return {"kernel": k, "bound": "valu", "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 4), "traffic": None,
-                    "launch_ms": round(ms, 4), "group_iterations_per_launch": int(group_iters),
-                    "useful_lane_fraction": round(frac_lanes, 4),
-                    "f64_lane_flops_per_group_iteration_all_lanes": v["f64_lane_flops_per_group_iteration"],
-                    "frac_all_lanes": round(ach / frac_lanes / PEAK_FP64_TFLOPS, 4),
-                    "algorithmic_flops_per_launch": fl, "source": SOLVE_PMC,
-                    "note": "FP64 VALU work of the lanes that hold a node (k <= N) only; the kernel is bound "
-                            "by the issue of each instance's serial chains, not by HBM (traffic = its "
-                            "inputs/outputs, see solve_kernel.hbm_frac)"}
-    return None
+            return (k, v), None
+    return None, f"no record for {kernel_substr} G={G} in {SOLVE_PMC}"
+
+
+def solve_roofline(kernel_substr, G, algo, group_iters, ms):
+    """Roofline entry of the fused solve kernel: algorithmic FP64 flops of the launch's IPM
+    iterations / the launch's HIP-event time / the FP64 vector peak, with the issued FP64
+    lane-flops of the committed PMC characterisation beside it (when current)."""
+    if algo is None or ms <= 0 or group_iters <= 0:
+        return None
+    fl = algo["per_iteration"] * group_iters
+    ach = fl / (ms * 1e-3) / 1e12
+    r = {"kernel": f"solve_kernel<{kernel_substr}..., G={G}>", "bound": "valu", "achieved": round(ach, 4),
+         "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 5), "traffic": None,
+         "launch_ms": round(ms, 4), "group_iterations_per_launch": int(group_iters),
+         "algorithmic_flops_per_group_iteration": round(algo["per_iteration"], 1),
+         "algorithmic_flops_per_node": algo["per_node"], "algorithmic_sources": [algo["eval_source"],
+                                                                                 algo["riccati_source"]],
+         "algorithmic_flops_per_launch": fl,
+         "note": "the kernel is bound by the issue of each instance's serial chains (one wave per SIMD), "
+                 "not by HBM (traffic = its inputs/outputs, see solve_kernel.hbm_frac) nor by FP64 throughput"}
+    pmc, why = load_solve_pmc(kernel_substr, G)
+    if pmc is None:
+        r["issued"] = why
+    else:
+        k, v = pmc
+        iss = v["f64_lane_flops_per_group_iteration"]
+        r["issued"] = {"kernel": k, "f64_lane_flops_per_group_iteration": round(iss, 1),
+                       "tflops": round(iss * group_iters / (ms * 1e-3) / 1e12, 3),
+                       "algorithmic_over_issued": round(algo["per_iteration"] / iss, 4), "source": SOLVE_PMC}
+    return r
 
 
 def sweep_roofline(solver, torch, B, N, reps, stream):
@@ -362,6 +443,7 @@ def main():
     torch.cuda.set_device(local)
     mdist.init(mdist.backend("nccl"))
     import mpcx
+    from mpcx import _lib
     from mpcx.device import DeviceLoop
 
     cfg = args.config
@@ -533,7 +615,10 @@ def main():
     else:
         run_ms, run_iters = float(np.sum(solve_ms)), int(lk_it.sum().item())
     kname = VARIANT_KERNEL[variant] if variant else CFG_KERNEL[cfg]
-    roof_solve = solve_roofline(kname, G, N + 1, run_iters, run_ms) if rank == 0 else None
+    algo, why_not = algorithmic_flops_per_iteration(variant or cfg, ocp, N)
+    roof_solve = solve_roofline(kname, G, algo, run_iters, run_ms) if rank == 0 else None
+    if rank == 0 and roof_solve is None:
+        roof_solve = {"kernel": kname, "unavailable": why_not or "no timed iterations"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and cfg == 2:
@@ -587,6 +672,7 @@ def main():
             "failed_instances": int((S_all[:, 3] > 1).sum()),
             "iters_sum_all_steps": int(iters_all),
             "roofline": roof_solve, "roofline_sweep": roof, "cpu_baseline": cpu, "solve_kernel": solve_info,
+            "mpcx_source_hash": _lib.source_hash(),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -554,7 +554,7 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
 // after the device is idle, since a queued launch may still use it)
 static int solve_launch(mpcx_handle* h, mpcx::SolveArgs& a, hipStream_t stream) {
   const int slots = mpcx::resto_ws_slots(a.model, a.nx, a.nu);
-  if (slots > 0 && a.restoration) {
+  if (slots > 0) {  // (the 6-state bicycle's chain stash needs it with restoration off too)
     const int G = mpcx::solve_group_size(a.N, a.B, a.n_simd, a.group_policy);
     const long bs = G > 64 ? G : 64;
     const long threads = ((long)a.B * G + bs - 1) / bs * bs;

@@ -99,6 +99,12 @@ __device__ __forceinline__ int iuw(int k, int i) {
   return NX + (NX + NU) * k + i;
 }
 
+// workspace load through the global address space (a global_load, not a flat load that might
+// alias the stack)
+__device__ __forceinline__ double wsload(const double* base, long i) {
+  return ((const __attribute__((address_space(1))) double*)base)[i];
+}
+
 // sum of log(slack) over the bounded components of a lane's variables as ONE log: the
 // product of the slacks' frexp mantissas (each in [0.5, 1), at most 2 NZ factors, so no
 // under/overflow) plus the exponents times ln 2.  One log instead of one per bound.
@@ -245,6 +251,11 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   __shared__ double sbuf[Model::kParallelRiccati ? RElem<NX>::NE * kSBS : 1];
   // LDS cache of the ODE models' transcendental values across their derivative passes (ode.h)
   __shared__ double tcache[Model::kTrigSlots > 0 ? Model::kTrigSlots * kSBS : 1];
+  // workspace chain stash (solver.h chain_ws_slots): slots after the restoration workspace's
+  constexpr bool kWsStash = WsStashOf<Model>::value;
+  constexpr int kWsH = RestoWs::slots(NX, NU);       // stage Hessian (NH), then Sigma (NZ)
+  constexpr int kWsA = kWsH + NH + NZ;                // A (NX^2), then B (NX NU), masked entries only
+  static_assert(!kWsStash || kWsA + NX * NX + NX * NU == kWsH + chain_ws_slots(NX, NU), "chain stash slots");
   XWave<G> xw{xch, 0};
   const int inst = (int)(gid / G);
   const bool valid = inst < a.B;
@@ -930,6 +941,36 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     STAMP(3);
     phase();
     // ------------------------------------------------------------ Riccati + inertia correction
+    // Models with a workspace chain stash (kernels.h WsStashOf: the 6-state bicycle) keep the
+    // stage Hessian and Sigma in the workspace instead of registers across the inertia-correction
+    // loop: every attempt re-reads them (node-parallel, coalesced), so neither is live across the
+    // sequential chain, whose operands then fit the registers (no scratch round trip per step)
+    if constexpr (kWsStash) {
+      double* wsl = a.ws + gid;
+      long wst = a.ws_stride;
+      asm volatile("" : "+v"(wsl), "+v"(wst));  // no workspace addresses hoisted out of the loop
+#pragma unroll
+      for (int i = 0; i < NH; ++i) wsl[(long)(kWsH + i) * wst] = Hs[i];
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) wsl[(long)(kWsH + NH + i) * wst] = sig[i];
+#pragma unroll
+      for (int i = 0; i < NX * NX; ++i)
+        if (Model::AMASK & (1ull << i)) wsl[(long)(kWsA + i) * wst] = A[i];
+#pragma unroll
+      for (int i = 0; i < NX * NU; ++i)
+        if (Model::BMASK & (1ull << i)) wsl[(long)(kWsA + NX * NX + i) * wst] = Bm[i];
+    }
+    // this lane's Jacobians back from the workspace (kWsStash), for the phases after the chain
+    auto ws_jac = [&](double* Aw, double* Bw) __attribute__((always_inline)) {
+      double* wsl = a.ws + gid;
+      long wst = a.ws_stride;
+      asm volatile("" : "+v"(wsl), "+v"(wst));
+#pragma unroll
+      for (int i = 0; i < NX * NX; ++i) Aw[i] = (Model::AMASK & (1ull << i)) ? wsload(wsl, (long)(kWsA + i) * wst) : 0.0;
+#pragma unroll
+      for (int i = 0; i < NX * NU; ++i)
+        Bw[i] = (Model::BMASK & (1ull << i)) ? wsload(wsl, (long)(kWsA + NX * NX + i) * wst) : 0.0;
+    };
     double delta = 0.0;
     bool need = !done;  // instance still needs a factorisation
     bool failed = false;
@@ -938,16 +979,28 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     for (int attempt = 0; attempt < 64; ++attempt) {
       if (!__any(need)) break;
       // node-parallel: stage Hessian + Sigma + delta (off the sequential path)
-      double Hd[NH];
+      double Hd[NH], sgv[NZ];
       // stage Hessian (table-Hessian models: 2 fs W of the stage table; none at node N)
       const double hsc = Model::kTableHess ? (hasU ? 2.0 * fs : 0.0) : 1.0;
-      const double* Hsrc = Model::hessW(ctx, Hs);
       const double* Aop = Model::jacA(ctx, A);
       const double* Bop = Model::jacB(ctx, Bm);
+      if constexpr (kWsStash) {
+        double* wsl = a.ws + gid;
+        long wst = a.ws_stride;
+        asm volatile("" : "+v"(wsl), "+v"(wst));
 #pragma unroll
-      for (int i = 0; i < NH; ++i) Hd[i] = Model::kTableHess ? hsc * Hsrc[i] : Hsrc[i];
+        for (int i = 0; i < NH; ++i) Hd[i] = wsload(wsl, (long)(kWsH + i) * wst);
 #pragma unroll
-      for (int i = 0; i < NZ; ++i) Hd[symix(i, i, NZ)] += sig[i] + delta;
+        for (int i = 0; i < NZ; ++i) sgv[i] = wsload(wsl, (long)(kWsH + NH + i) * wst);
+      } else {
+        const double* Hsrc = Model::hessW(ctx, Hs);
+#pragma unroll
+        for (int i = 0; i < NH; ++i) Hd[i] = Model::kTableHess ? hsc * Hsrc[i] : Hsrc[i];
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) sgv[i] = sig[i];
+      }
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) Hd[symix(i, i, NZ)] += sgv[i] + delta;
 
       // backward sweep: node N .. 0 (value function moves lane k+1 -> k)
       double P[NP], p[NX];
@@ -967,7 +1020,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
 #pragma unroll
-              for (int j = i; j < NX; ++j) e.J[symix(i, j, NX)] = (i == j) ? sig[i] + delta : 0.0;
+              for (int j = i; j < NX; ++j) e.J[symix(i, j, NX)] = (i == j) ? sgv[i] + delta : 0.0;
               e.p[i] = gp[i];
             }
           }
@@ -993,7 +1046,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
 #pragma unroll
-          for (int j = i; j < NX; ++j) P[symix(i, j, NX)] = (i == j) ? dl * (sig[i] + delta) : 0.0;
+          for (int j = i; j < NX; ++j) P[symix(i, j, NX)] = (i == j) ? dl * (sgv[i] + delta) : 0.0;
           p[i] = dl * gp[i];
         }
         double dev = 0.0, mag = 1.0;
@@ -1047,7 +1100,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
           for (int i = 0; i < NX; ++i) {
 #pragma unroll
-            for (int j = i; j < NX; ++j) P[symix(i, j, NX)] = (i == j) ? dl * (sig[i] + delta) : 0.0;
+            for (int j = i; j < NX; ++j) P[symix(i, j, NX)] = (i == j) ? dl * (sgv[i] + delta) : 0.0;
             p[i] = dl * gp[i];
           }
         }
@@ -1091,6 +1144,26 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
                   okl = riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec, AOneOf<Model>::value>(
                       Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p, fac);
                 }
+              } else if constexpr (kWsStash) {
+                // this step's operands from the workspace (lane j only): no lane keeps its stage
+                // Hessian and Jacobians in registers across the chain
+                double Hj[NH], Aj[NX * NX], Bj[NX * NU];
+                ws_jac(Aj, Bj);
+                {
+                  double* wsl = a.ws + gid;
+                  long wst = a.ws_stride;
+                  asm volatile("" : "+v"(wsl), "+v"(wst));
+#pragma unroll
+                  for (int i = 0; i < NZ; ++i)
+#pragma unroll
+                    for (int jj = i; jj < NZ; ++jj) {
+                      const int t = symix(i, jj, NZ);
+                      Hj[t] = wsload(wsl, (long)(kWsH + t) * wst);
+                      if (jj == i) Hj[t] += wsload(wsl, (long)(kWsH + NH + i) * wst) + delta;
+                    }
+                }
+                (void)riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec, AOneOf<Model>::value>(
+                    Hj, gp, Aj, Bj, cdef, Pin_, pin_, P, p, fac);
               } else {
                 (void)riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec, AOneOf<Model>::value>(
                     Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p, fac);
@@ -1199,19 +1272,27 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       // closed-loop map of the step, node-parallel (off the sequential chain):
       // dx_{k+1} = (A + B K) dx_k + (c + B k_f);  du_k = k_f + K dx_k afterwards
       double Acl[NX * NX], ccl[NX];
+      double Aw_[kWsStash ? NX * NX : 1], Bw_[kWsStash ? NX * NU : 1];
+      const double* Af_ = Model::jacA(ctx, A);
+      const double* Bf_ = Model::jacB(ctx, Bm);
+      if constexpr (kWsStash) {
+        ws_jac(Aw_, Bw_);
+        Af_ = Aw_;
+        Bf_ = Bw_;
+      }
 #pragma unroll
       for (int r = 0; r < NX; ++r) {
         double acc = cc_[r];
 #pragma unroll
         for (int l = 0; l < NU; ++l)
-          if (Model::BMASK & (1ull << (r * NU + l))) acc = fma(Model::jacB(ctx, Bm)[r * NU + l], kf_[l], acc);
+          if (Model::BMASK & (1ull << (r * NU + l))) acc = fma(Bf_[r * NU + l], kf_[l], acc);
         ccl[r] = acc;
 #pragma unroll
         for (int m = 0; m < NX; ++m) {
-          double e = (Model::AMASK & (1ull << (r * NX + m))) ? Model::jacA(ctx, A)[r * NX + m] : 0.0;
+          double e = (Model::AMASK & (1ull << (r * NX + m))) ? Af_[r * NX + m] : 0.0;
 #pragma unroll
           for (int l = 0; l < NU; ++l)
-            if (Model::BMASK & (1ull << (r * NU + l))) e = fma(Model::jacB(ctx, Bm)[r * NU + l], Kk[l * NX + m], e);
+            if (Model::BMASK & (1ull << (r * NU + l))) e = fma(Bf_[r * NU + l], Kk[l * NX + m], e);
           Acl[r * NX + m] = e;
         }
       }
@@ -1704,6 +1785,12 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
             auto soc_step = [&](const double* pin) __attribute__((always_inline)) {
               const double* Aop = Model::jacA(ctx, A);
               const double* Bop = Model::jacB(ctx, Bm);
+              double Aw_[kWsStash ? NX * NX : 1], Bw_[kWsStash ? NX * NU : 1];
+              if constexpr (kWsStash) {
+                ws_jac(Aw_, Bw_);
+                Aop = Aw_;
+                Bop = Bw_;
+              }
               double sv[NX], gu[NU];
 #pragma unroll
               for (int i = 0; i < NX; ++i) {

@@ -35,6 +35,9 @@
 #ifndef MPCX_ODE_RESTO
 #define MPCX_ODE_RESTO true
 #endif
+#ifndef MPCX_WS_STASH
+#define MPCX_WS_STASH true
+#endif
 
 namespace mpcx {
 
@@ -273,6 +276,10 @@ struct OdeModel {
   // IPOPT's soft restoration and feasibility restoration phase (kernels.h; state in the
   // restoration workspace): the nonlinear models are the ones whose line searches fail
   static constexpr bool kResto = MPCX_ODE_RESTO;
+  // stage Hessian and Sigma of the 6-state model wait in the workspace across the inertia-
+  // correction loop (kernels.h kWsStash): with them out of the registers the sequential chain's
+  // operands no longer go through scratch once per step
+  static constexpr bool kWsStash = MPCX_WS_STASH && NX >= 6;
   static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT && NX <= 5;  // NX = 6: LDS buffer too large
   struct Ctx {
     double zr[NZ];

@@ -17,8 +17,10 @@
 
 namespace mpcx {
 
-// packed upper-triangular index of a symmetric n x n matrix
-__host__ __device__ constexpr int symix(int i, int j, int n) {
+// packed upper-triangular index of a symmetric n x n matrix.  Always inlined: in the largest
+// kernels (the 6-state bicycle) the inliner otherwise leaves it a call, its index a run-time
+// value, and every array it indexes a stack object in scratch.
+__host__ __device__ constexpr __forceinline__ int symix(int i, int j, int n) {
   return i <= j ? i * n - i * (i - 1) / 2 + (j - i) : j * n - j * (j - 1) / 2 + (i - j);
 }
 
@@ -69,6 +71,16 @@ struct XBoundsOf {
 template <class M>
 struct XBoundsOf<M, std::void_t<decltype(M::kXBounds)>> {
   static constexpr bool value = M::kXBounds;
+};
+// model trait: the stage Hessian and Sigma wait in the restoration workspace across the
+// inertia-correction loop (kernels.h kWsStash; solver.h chain_ws_slots sizes the slots)
+template <class M, class = void>
+struct WsStashOf {
+  static constexpr bool value = false;
+};
+template <class M>
+struct WsStashOf<M, std::void_t<decltype(M::kWsStash)>> {
+  static constexpr bool value = M::kWsStash;
 };
 
 // AONE: bit r*NX+j set = A[r][j] is exactly 1 (a model's structural unit entries, within AMASK):

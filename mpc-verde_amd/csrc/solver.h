@@ -132,7 +132,12 @@ struct RestoWs {
   __host__ __device__ static constexpr int SC(int nx, int nz) { return 6 * nz + 3 * nx; }
   __host__ __device__ static constexpr int slots(int nx, int nu) { return SC(nx, nx + nu) + kScalars; }
 };
-// doubles of restoration workspace per thread (0: the model has no restoration phase)
+// workspace chain stash of the models with kWsStash (the 6-state bicycle, model 4): the stage
+// Hessian (packed), Sigma, A and B of every lane, after the restoration slots
+__host__ __device__ constexpr int chain_ws_slots(int nx, int nu) {
+  return (nx + nu) * (nx + nu + 1) / 2 + nx + nu + nx * nx + nx * nu;
+}
+// doubles of workspace per thread (restoration + chain stash; 0: the model uses none)
 int resto_ws_slots(int model, int nx, int nu);
 
 hipError_t launch_solve(const SolveArgs& a, hipStream_t stream);

@@ -88,10 +88,11 @@ hipError_t launch_rk4_sens(int B, int N, const StageParams& sp, const double* X,
   return hipGetLastError();
 }
 
-// restoration workspace per thread: the ODE models (kernels.h RestoWs); none elsewhere
+// workspace per thread: restoration (kernels.h RestoWs) for the unicycle and the ODE models, plus
+// the chain stash of the 6-state bicycle; none elsewhere
 int resto_ws_slots(int model, int nx, int nu) {
   if (model != 1 && (model < 3 || model > 5)) return 0;  // the models with kResto: unicycle (1), ODE (3-5)
-  return RestoWs::slots(nx, nu);
+  return RestoWs::slots(nx, nu) + (model == 4 ? chain_ws_slots(nx, nu) : 0);  // model 4: OdeModel<DynBicycle>::kWsStash
 }
 
 // ---- model dispatch (the entry points live in solve_<model>.hip) -------------------

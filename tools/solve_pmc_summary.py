@@ -1,6 +1,11 @@
 """Summarise tools/solve_pmc.sh: per-dispatch averages over the solve_kernel dispatches.
 
-    python tools/solve_pmc_summary.py gpurun_out/solve_pmc > profiles/r02_solve_kernel_pmc.json
+    python tools/solve_pmc_summary.py gpurun_out/solve_pmc/c2 [more run dirs ...] > profiles/r03_solve_kernel_pmc.json
+
+Several run directories (one per workload, tools/solve_pmc_all.sh) merge into one record per
+kernel.  "_meta.mpcx_source_hash" is the source hash of the library the runs measured (from
+the bench lines of the pass logs; all runs must agree): bench.py uses a record only while the
+tree's sources still hash to it.
 
 SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles summed over waves
 (MI355X_MICROARCH.md, PMC units); WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES.
@@ -35,15 +40,20 @@ def counters(d):
             for k, cs in agg.items()}
 
 
-def bench_iters(log):
-    """iters_sum_all_steps of the bench JSON line in a pass log."""
+def bench_line(log):
+    """The bench JSON line of a pass log (or {})."""
     try:
         for line in open(log):
             if line.startswith("{") and "iters_sum_all_steps" in line:
-                return json.loads(line)["iters_sum_all_steps"]
+                return json.loads(line)
     except OSError:
         pass
-    return None
+    return {}
+
+
+def bench_iters(log):
+    """iters_sum_all_steps of the bench JSON line in a pass log."""
+    return bench_line(log).get("iters_sum_all_steps")
 
 
 def durations(d):
@@ -55,8 +65,7 @@ def durations(d):
     return out
 
 
-def main():
-    root = sys.argv[1]
+def summarise(root):
     a, b, tr = counters(os.path.join(root, "a")), counters(os.path.join(root, "b")), durations(os.path.join(root, "trace"))
     res = {}
     for k in a:
@@ -83,8 +92,24 @@ def main():
         if t:
             r["fp64_tflops"] = round(flops / t / 1e12, 3)
             r["fp64_frac_of_peak"] = round(flops / t / 1e12 / PEAK_FP64_TFLOPS, 4)
+        r["workload"] = bench_line(os.path.join(root, "b.log")).get("config", {}).get("workload")
         res[k] = r
-    print(json.dumps(res, indent=1))
+    return res
+
+
+def main():
+    res, hashes = {}, set()
+    for root in sys.argv[1:]:
+        res.update(summarise(root))
+        for p in ("a", "b", "trace"):
+            h = bench_line(os.path.join(root, f"{p}.log")).get("mpcx_source_hash")
+            if h:
+                hashes.add(h)
+    if len(hashes) != 1:
+        raise SystemExit(f"runs disagree on (or lack) the library source hash: {sorted(hashes)}")
+    out = {"_meta": {"mpcx_source_hash": hashes.pop(), "runs": sys.argv[1:]}}
+    out.update(res)
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
