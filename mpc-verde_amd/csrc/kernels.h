@@ -225,6 +225,9 @@ struct LdsCol {
   __device__ __forceinline__ void relaunder() { asm volatile("" : "+v"(off)); }
 };
 
+#ifndef MPCX_DEC_TIGHT
+#define MPCX_DEC_TIGHT 1
+#endif
 #ifndef MPCX_SOFT_INLINE
 #define MPCX_SOFT_INLINE true
 #endif
@@ -1121,12 +1124,34 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
             for (int i = 0; i < NP; ++i) P[i] = Pk[i];
           }
         }
+        // steps j >= jc are reused-suffix steps for every group of the wave: they run first, in
+        // a loop of their own that moves only p (the same operations as the mixed loop's cheap
+        // steps; A stays in the stage table: 25 more live registers here measured slower)
+        int jc = N;
+        if constexpr (kDec && MPCX_DEC_TIGHT) {
+          if (__all(reuse)) {
+            XWave<64> xw1{nullptr, 0};
+            jc = G >= 64 ? kb : (int)greduce<64, OpMax>((double)kb, xw1);  // max over the wave's groups
+            jc = __builtin_amdgcn_readfirstlane(jc);  // wave-uniform: scalar loop bounds
+          }
+        }
         if constexpr (G <= 64) {
+          if constexpr (kDec) {
+            for (int j = N - 1; j >= jc; --j) {
+              double pin_[NX];
+#pragma unroll
+              for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
+              if (seq && k == j) {
+                dec_vector_step<NX, NU, Model::AMASK, Model::BMASK>(gp, Aop, Bop, vpc, pin_, p, fac);
+                okl = okd;
+              }
+            }
+          }
           // the chain: one step per node, lane j only.  Models without the decoupled suffix take
           // the inertia verdict of their step from its factors after the chain, on all lanes at
           // once (fac_ok), so no lane-mask merge sits on the chain
 #pragma unroll 2
-          for (int j = N - 1; j >= 0; --j) {
+          for (int j = min(N, jc) - 1; j >= 0; --j) {
             const bool cheap = reuse && j >= kb;
             double Pin_[NP], pin_[NX];
             if (!kDec || __any(!cheap)) {
@@ -1178,7 +1203,21 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
             if (wv == ph) {
               const double* in = xw.prev();  // (P, p) of node 64 (ph + 1), written last phase
               const int jtop = 64 * ph + 63;
-              for (int j = min(N - 1, jtop); j >= 64 * ph; --j) {
+              if constexpr (kDec) {  // this wave's reused-suffix steps (see jc above)
+                for (int j = min(N - 1, jtop); j >= max(jc, 64 * ph); --j) {
+                  double pin_[NX];
+#pragma unroll
+                  for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);
+                  if (j == jtop && lane == 63)
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) pin_[i] = in[NP + i];
+                  if (seq && k == j) {
+                    dec_vector_step<NX, NU, Model::AMASK, Model::BMASK>(gp, Aop, Bop, vpc, pin_, p, fac);
+                    okl = okd;
+                  }
+                }
+              }
+              for (int j = min(min(N - 1, jtop), jc - 1); j >= 64 * ph; --j) {
                 const bool cheap = reuse && j >= kb;
                 double Pin_[NP], pin_[NX];
                 if (!kDec || __any(!cheap)) {
