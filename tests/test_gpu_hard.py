@@ -4,10 +4,11 @@
 * the unicycle NLP of Casadi/multiple_shooting_casadi.py at N = 20 on non-convex instances:
   headings over the whole circle, targets behind and beside the vehicle, targets at distance
   ~0 and exactly 0, target headings a half turn away (SURVEY.md §7 hard part 3: turn left vs
-  right).  The kernel has no restoration phase for the unicycle; the oracle runs with IPOPT's
-  restoration phase ON, so a kernel instance ending where IPOPT would have restored shows up as
-  a status difference.  Statuses, iteration counts and optima are compared instance by
-  instance (counts printed, bounded; a differing optimum must be a KKT point);
+  right).  Both sides run IPOPT's restoration (the kernel: the soft restoration step inline and
+  the restoration phase in the resume launch, csrc/resto.h; the oracle: ipm_ref.cpp's), so an
+  instance one side restores and the other does not shows up as a status or iteration
+  difference.  Statuses, iteration counts and optima are compared instance by instance (counts
+  printed; 0 differ);
 * the same starts through the device closed loop (multi-step launch == lock-step launches);
 * IPOPT's park-and-resume path (restoration in a second launch, resto.h) through DeviceLoop:
   the fused step epilogue and multi-step launches with parked instances, bit for bit against
