@@ -17,10 +17,13 @@ owns B instances; no collective inside the timed region.
 Printed JSON (rank 0): value = total solves/s over all ranks; ms_per_step = the
 max-over-ranks wall time per step; ms_per_solve_p50 = median batched solve-call
 latency (HIP events).  `roofline` describes the kernel that dominates the timed
-region, the fused solve_kernel: useful FP64 flops per launch (PMC FP64
-lane-flops per group-iteration, profiles/r02_solve_kernel_pmc.json, x the
-fraction of lanes that hold a node, x this launch's group-iterations) / the
-launch's HIP-event time / the FP64 vector peak.  `roofline_sweep` describes the
+region, the fused solve_kernel: algorithmic FP64 flops per launch (the flops one
+IPM iteration of one instance needs -- per-node evaluation and Riccati step
+measured by tools/flop_probe.py, profiles/r03_flop_probe.json, plus the IPM's
+vector work counted in ipm_vector_flops; DESIGN.md §6 -- x the launch's
+instance-iterations) / the launch's HIP-event time / the FP64 vector peak, with
+the issued FP64 lane-flops of profiles/r03_solve_kernel_pmc.json beside it while
+that record matches the library's source hash.  `roofline_sweep` describes the
 RK4 + Jacobian sweep kernel (rk4_sens, the HBM-streaming kernel of SURVEY.md
 §8(d)) at B = 2^19, N = 20.  `cpu_baseline` times the C++ CPU oracle
 (oracle/ipm_ref.cpp, kind "port") on every CPU the process may use, on a

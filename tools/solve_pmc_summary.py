@@ -107,7 +107,8 @@ def main():
                 hashes.add(h)
     if len(hashes) != 1:
         raise SystemExit(f"runs disagree on (or lack) the library source hash: {sorted(hashes)}")
-    out = {"_meta": {"mpcx_source_hash": hashes.pop(), "runs": sys.argv[1:]}}
+    root = os.environ.get("GRAFT_REPO_ROOT", os.getcwd())
+    out = {"_meta": {"mpcx_source_hash": hashes.pop(), "runs": [os.path.relpath(r, root) for r in sys.argv[1:]]}}
     out.update(res)
     print(json.dumps(out, indent=1))
 
