@@ -256,9 +256,20 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   __shared__ double tcache[Model::kTrigSlots > 0 ? Model::kTrigSlots * kSBS : 1];
   // workspace chain stash (solver.h chain_ws_slots): slots after the restoration workspace's
   constexpr bool kWsStash = WsStashOf<Model>::value;
-  constexpr int kWsH = RestoWs::slots(NX, NU);       // stage Hessian (NH), then Sigma (NZ)
-  constexpr int kWsA = kWsH + NH + NZ;                // A (NX^2), then B (NX NU), masked entries only
-  static_assert(!kWsStash || kWsA + NX * NX + NX * NU == kWsH + chain_ws_slots(NX, NU), "chain stash slots");
+  // The stash is one contiguous record per thread (array of structures, after the restoration
+  // workspace's slot-major part): the chain's single active lane then reads its operands from
+  // a few cache lines in 16-byte loads instead of one line per value.
+  constexpr int kWsH = RestoWs::slots(NX, NU);  // slot-major slots before the records
+  constexpr int kCS = chain_ws_slots(NX, NU);   // record: stage Hessian (NH), Sigma (NZ), A (NX^2), B (NX NU)
+  constexpr int kRH = 0, kRS = NH, kRA = NH + NZ, kRB = NH + NZ + NX * NX;
+  static_assert(!kWsStash || (kRB + NX * NU == kCS && kCS % 2 == 0), "chain stash record");
+  // this thread's record (16-byte aligned: hipMalloc base, 64-thread-multiple stride, even kCS);
+  // opaque, so no address is hoisted out of the solve loop
+  auto wsrec = [&]() __attribute__((always_inline)) -> const double* {
+    double* r = a.ws + (long)kWsH * a.ws_stride + gid * kCS;
+    asm volatile("" : "+v"(r));
+    return (const double*)__builtin_assume_aligned(r, 16);
+  };
   XWave<G> xw{xch, 0};
   const int inst = (int)(gid / G);
   const bool valid = inst < a.B;
@@ -949,30 +960,23 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     // loop: every attempt re-reads them (node-parallel, coalesced), so neither is live across the
     // sequential chain, whose operands then fit the registers (no scratch round trip per step)
     if constexpr (kWsStash) {
-      double* wsl = a.ws + gid;
-      long wst = a.ws_stride;
-      asm volatile("" : "+v"(wsl), "+v"(wst));  // no workspace addresses hoisted out of the loop
+      double* r = const_cast<double*>(wsrec());
 #pragma unroll
-      for (int i = 0; i < NH; ++i) wsl[(long)(kWsH + i) * wst] = Hs[i];
+      for (int i = 0; i < NH; ++i) r[kRH + i] = Hs[i];
 #pragma unroll
-      for (int i = 0; i < NZ; ++i) wsl[(long)(kWsH + NH + i) * wst] = sig[i];
+      for (int i = 0; i < NZ; ++i) r[kRS + i] = sig[i];
 #pragma unroll
-      for (int i = 0; i < NX * NX; ++i)
-        if (Model::AMASK & (1ull << i)) wsl[(long)(kWsA + i) * wst] = A[i];
+      for (int i = 0; i < NX * NX; ++i) r[kRA + i] = (Model::AMASK & (1ull << i)) ? A[i] : 0.0;
 #pragma unroll
-      for (int i = 0; i < NX * NU; ++i)
-        if (Model::BMASK & (1ull << i)) wsl[(long)(kWsA + NX * NX + i) * wst] = Bm[i];
+      for (int i = 0; i < NX * NU; ++i) r[kRB + i] = (Model::BMASK & (1ull << i)) ? Bm[i] : 0.0;
     }
     // this lane's Jacobians back from the workspace (kWsStash), for the phases after the chain
     auto ws_jac = [&](double* Aw, double* Bw) __attribute__((always_inline)) {
-      double* wsl = a.ws + gid;
-      long wst = a.ws_stride;
-      asm volatile("" : "+v"(wsl), "+v"(wst));
+      const double* r = wsrec();
 #pragma unroll
-      for (int i = 0; i < NX * NX; ++i) Aw[i] = (Model::AMASK & (1ull << i)) ? wsload(wsl, (long)(kWsA + i) * wst) : 0.0;
+      for (int i = 0; i < NX * NX; ++i) Aw[i] = (Model::AMASK & (1ull << i)) ? wsload(r, kRA + i) : 0.0;
 #pragma unroll
-      for (int i = 0; i < NX * NU; ++i)
-        Bw[i] = (Model::BMASK & (1ull << i)) ? wsload(wsl, (long)(kWsA + NX * NX + i) * wst) : 0.0;
+      for (int i = 0; i < NX * NU; ++i) Bw[i] = (Model::BMASK & (1ull << i)) ? wsload(r, kRB + i) : 0.0;
     };
     double delta = 0.0;
     bool need = !done;  // instance still needs a factorisation
@@ -988,13 +992,11 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       const double* Aop = Model::jacA(ctx, A);
       const double* Bop = Model::jacB(ctx, Bm);
       if constexpr (kWsStash) {
-        double* wsl = a.ws + gid;
-        long wst = a.ws_stride;
-        asm volatile("" : "+v"(wsl), "+v"(wst));
+        const double* r = wsrec();
 #pragma unroll
-        for (int i = 0; i < NH; ++i) Hd[i] = wsload(wsl, (long)(kWsH + i) * wst);
+        for (int i = 0; i < NH; ++i) Hd[i] = wsload(r, kRH + i);
 #pragma unroll
-        for (int i = 0; i < NZ; ++i) sgv[i] = wsload(wsl, (long)(kWsH + NH + i) * wst);
+        for (int i = 0; i < NZ; ++i) sgv[i] = wsload(r, kRS + i);
       } else {
         const double* Hsrc = Model::hessW(ctx, Hs);
 #pragma unroll
@@ -1175,16 +1177,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
                 double Hj[NH], Aj[NX * NX], Bj[NX * NU];
                 ws_jac(Aj, Bj);
                 {
-                  double* wsl = a.ws + gid;
-                  long wst = a.ws_stride;
-                  asm volatile("" : "+v"(wsl), "+v"(wst));
+                  const double* r = wsrec();
 #pragma unroll
                   for (int i = 0; i < NZ; ++i)
 #pragma unroll
                     for (int jj = i; jj < NZ; ++jj) {
                       const int t = symix(i, jj, NZ);
-                      Hj[t] = wsload(wsl, (long)(kWsH + t) * wst);
-                      if (jj == i) Hj[t] += wsload(wsl, (long)(kWsH + NH + i) * wst) + delta;
+                      Hj[t] = wsload(r, kRH + t);
+                      if (jj == i) Hj[t] += wsload(r, kRS + i) + delta;
                     }
                 }
                 (void)riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, kDec, AOneOf<Model>::value>(
