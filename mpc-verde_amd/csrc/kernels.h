@@ -537,7 +537,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     for (int i = 0; i < NX; ++i) own[NZ + i] = lam[i] / fs;
     group_next<G, NS>(own, nxt, xw);
     if (bnd) {
-      if (k == 0) {
+      if (k == 0 && valid) {  // lanes past the batch are done from the start: no status row of theirs
         if (a.status) a.status[(size_t)step * a.B + inst] = status;
         if (a.iters) a.iters[(size_t)step * a.B + inst] = its;
         double zp[NZ], xfp[NX], qp;
@@ -550,13 +550,14 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         for (int i = 0; i < NX; ++i) x0[i] = xfp[i];
       }
       ++step;
-      const double* Pn = a.Pseq ? a.Pseq + ((size_t)step * a.B + inst) * a.p_stride : Pin;
+      const int ivi = valid ? inst : 0;  // never index past the batch
+      const double* Pn = a.Pseq ? a.Pseq + ((size_t)step * a.B + ivi) * a.p_stride : Pin;
       ModelArgs mst = ma;
       if (a.tabseq) {
         mst.lin.tab = a.tabseq + (size_t)step * a.B * N;
         mst.lin.per_instance = 1;
       }
-      Model::load_ctx(mst, inst, Pn, k, hasU, ctx);
+      Model::load_ctx(mst, ivi, Pn, k, hasU, ctx);
       const bool lastX = (k == N), lastU = (k == N - 1);
       warm = a.warm_next != 0;
 #pragma unroll
@@ -2279,6 +2280,8 @@ static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
   // wave): the per-wave instruction stream is the same, but a wave then runs only its own
   // instance's iterations, not the maximum over the instances it holds (config 2: +5 %
   // solves/s in multi-step launches).  spec.group_policy = 1 keeps the narrowest group.
+  // (Measured and not adopted: collectives over the 32 lanes of config 2's nodes on the same
+  // 64-lane grid -- no gain)
   const int G = solve_group_size(a.N, a.B, a.n_simd, a.group_policy);
   const long threads = (long)a.B * G;
   const int bs = G > 64 ? G : 64;

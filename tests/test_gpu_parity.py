@@ -716,6 +716,39 @@ def test_run_tracking_with_stage_reference_sequence(mpcx):
     np.testing.assert_array_equal(b["P"][:, 0:3], a["P"][:, 0:3])  # x0 (run keeps step-0 refs in P)
 
 
+def test_run_ragged_last_wave_with_reference_sequence(mpcx):
+    """Multi-step launch whose last wave holds lanes of no instance (narrowest groups: 4 instances
+    per wave at N = 10, B = 37): those lanes are done from the start and must neither write a
+    status row nor read per-step references past the batch -- run == lock-step, bit for bit."""
+    import torch
+    from mpcx import dist
+    from mpcx.device import DeviceLoop
+
+    N, B, K = 10, 37, 4
+    tau0, P0 = dist.config3_inputs(0, B, N=N)
+    solver = mpcx.nlpsol("t", "mi355x", mpcx.unicycle_tracking(N=N), {"group_policy": 1})
+    refs = np.stack([mpcx.ocp.circular_reference(tau0, t, N).reshape(B, -1) for t in range(K)])
+    Pseq = np.zeros((K, B, P0.shape[1]))
+    Pseq[:, :, 3:] = refs
+    lock = DeviceLoop(solver, P0)
+    run = DeviceLoop(solver, P0)
+    dr = torch.from_numpy(refs).cuda()
+    st_l, it_l = [], []
+    for t in range(K):
+        lock.set_stage_refs(dr[t])
+        lock.step()
+        torch.cuda.synchronize()
+        st_l.append(lock.status.cpu().numpy().copy())
+        it_l.append(lock.iters.cpu().numpy().copy())
+    st_r, it_r = run.run(K, Pseq=torch.from_numpy(Pseq).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st_r.cpu().numpy(), np.array(st_l))
+    np.testing.assert_array_equal(it_r.cpu().numpy(), np.array(it_l))
+    a, b = _state(lock), _state(run)
+    for n in ("w", "w0", "lam0", "lamx0", "f"):
+        np.testing.assert_array_equal(b[n], a[n], err_msg=n)
+
+
 def test_run_ltv_with_schedule_sequence(mpcx):
     """Config-4 LTV: per-step references (Pseq) and schedules (tabseq) == the lock-step loop."""
     import torch
