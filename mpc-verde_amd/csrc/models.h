@@ -23,6 +23,9 @@
 #ifndef MPCX_BOUNDS_LDS
 #define MPCX_BOUNDS_LDS false
 #endif
+#ifndef MPCX_BOUNDS_LDS_LIN
+#define MPCX_BOUNDS_LDS_LIN true
+#endif
 #ifndef MPCX_UNI_MOMENTS
 #define MPCX_UNI_MOMENTS true
 #endif
@@ -136,6 +139,11 @@ struct LinearModel {
   // decoupled stages -- the move-blocked stages of the cart-pole QP (lti.py).  Scan models
   // keep their scan.
   static constexpr bool kDecSuffix = !kScan;
+  // variable bounds in LDS (kernels.h LdsCol), re-read per phase, instead of 2 NZ doubles of
+  // registers held through every phase: A/B on one MI355X, config 5 (LinearModel<5,1>, G = 128)
+  // scratch 704 -> 240 B/lane, 116 -> 100 us per IPM iteration (+15 % solves/s); config 4
+  // (LinearModel<4,1>, scan) +3.5 %, scratch 404 -> 0 (LinearModel<4,2>: 680 -> 84)
+  static constexpr bool kBoundsLds = MPCX_BOUNDS_LDS_LIN;
   static constexpr int kTrigSlots = 0;
   __device__ __forceinline__ static const double* jacA(const Ctx& c, const double* A) { return kTableJac ? c.A : A; }
   __device__ __forceinline__ static const double* jacB(const Ctx& c, const double* B) { return kTableJac ? c.B : B; }

@@ -35,6 +35,9 @@
 #ifndef MPCX_ODE_RESTO
 #define MPCX_ODE_RESTO true
 #endif
+#ifndef MPCX_BOUNDS_LDS_ODE
+#define MPCX_BOUNDS_LDS_ODE true
+#endif
 #ifndef MPCX_WS_STASH
 #define MPCX_WS_STASH true
 #endif
@@ -280,6 +283,11 @@ struct OdeModel {
   // correction loop (kernels.h kWsStash): with them out of the registers the sequential chain's
   // operands no longer go through scratch once per step
   static constexpr bool kWsStash = MPCX_WS_STASH && NX >= 6;
+  // variable bounds in LDS (kernels.h LdsCol) instead of 2 NZ doubles of registers held through
+  // every phase.  A/B on one MI355X: cart-pole swing-up 122 -> 117 us per IPM iteration (scratch
+  // 696 -> 204 B/lane), kinematic bicycle +1 % (scratch 400 -> 0); the 6-state bicycle, whose chain operands
+  // already wait in the workspace, 3 % slower -- so not there
+  static constexpr bool kBoundsLds = MPCX_BOUNDS_LDS_ODE && NX < 6;
   static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT && NX <= 5;  // NX = 6: LDS buffer too large
   struct Ctx {
     double zr[NZ];
