@@ -81,12 +81,15 @@ def compare(name, ocp, P, r, ref, nx, nz, max_differ, max_iter_differ):
 def test_config4_dyn_bicycle_batch_vs_ipopt_oracle(mpcx, C):
     """BASELINE config 4 as named: 6-state dynamic bicycle, lane_change.csv reference, N = 50, the
     bench's 1024 instances, cold start (X_k = x0, U = 0) in both.  100 % status <= 1 (before the
-    restoration phase 3 of these ended in a failed line search)."""
+    restoration phase 3 of these ended in a failed line search).  The bounds are the measured
+    counts (the kernel is deterministic): 5 optima differ, each KKT-certified, and 108 iteration
+    counts, from rounding growth between the hyper-dual and jet derivatives (DESIGN §6,
+    tools/divergence.py) -- any further drift fails the test."""
     ocp, P = config4_batch(mpcx)
     solver = mpcx.nlpsol("dyn", "mi355x", ocp, {"ipopt": {"max_iter": 3000}})
     r = solver.solve_batch(P)
     ref = C.solve(ocp, P, nthreads=0)
-    compare("config 4 dyn bicycle N=50", ocp, P, r, ref, 6, 8, max_differ=8, max_iter_differ=120)
+    compare("config 4 dyn bicycle N=50", ocp, P, r, ref, 6, 8, max_differ=5, max_iter_differ=108)
     assert np.min(r["w"][:, 6 + 2 + 3::8]) >= 2.5 - 1e-7  # vx >= 2.5 holds on X_1..X_N (stage k: U_k, X_k+1)
 
 
@@ -109,7 +112,7 @@ def test_config5_single_shooting_swingup_N100(mpcx, C):
     solver = mpcx.nlpsol("ss", "mi355x", ocp, {"ipopt": {"max_iter": 3000}})
     r = solver.solve_batch(P, w0)
     ref = C.solve(ocp, P, w0=w0, nthreads=0)
-    compare("config 5 single-shooting swing-up N=100", ocp, P, r, ref, 4, 5, max_differ=3, max_iter_differ=13)
+    compare("config 5 single-shooting swing-up N=100", ocp, P, r, ref, 4, 5, max_differ=0, max_iter_differ=0)
     for b in range(3):  # the CasADi-shaped call: decision U, g = X_1..X_N
         sol = solver(x0=[0.0] * N, lbx=-200.0, ubx=200.0, lbg=-math.inf, ubg=math.inf, p=P[b])
         assert solver.stats()["success"]
@@ -149,7 +152,7 @@ def test_kin_bicycle_iteration_counts_vs_oracle(mpcx, C):
     _, P = mdist.config3_bicycle_inputs(0, 1024, N=30)
     r = mpcx.nlpsol("kin", "mi355x", ocp, {"ipopt": {"max_iter": 3000}}).solve_batch(P)
     ref = C.solve(ocp, P, nthreads=0)
-    compare("config 3 kinematic bicycle N=30", ocp, P, r, ref, 3, 5, max_differ=10, max_iter_differ=20)
+    compare("config 3 kinematic bicycle N=30", ocp, P, r, ref, 3, 5, max_differ=0, max_iter_differ=0)
 
 
 def test_acceptable_level_termination_matches_oracle(mpcx, C):
