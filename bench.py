@@ -340,6 +340,14 @@ def solve_roofline(kernel_substr, G, algo, group_iters, ms):
         r["issued"] = {"kernel": k, "f64_lane_flops_per_group_iteration": round(iss, 1),
                        "tflops": round(iss * group_iters / (ms * 1e-3) / 1e12, 3),
                        "algorithmic_over_issued": round(algo["per_iteration"] / iss, 4), "source": SOLVE_PMC}
+        # the bound named above: with one wave per SIMD, the share of the wave's cycles in which it
+        # issues an instruction is the kernel's fraction of its issue ceiling (1.0)
+        wc = v.get("wave_cycles_share") or {}
+        if "issuing" in wc:
+            r["issue"] = {"issuing_share_of_wave_cycles": wc["issuing"],
+                          "waitcnt_or_barrier_share": wc.get("waitcnt_or_barrier"),
+                          "dependency_or_pipe_stall_share": wc.get("dependency_or_pipe_stall"),
+                          "valu_active_share": v.get("valu_active_share"), "source": SOLVE_PMC}
     return r
 
 
