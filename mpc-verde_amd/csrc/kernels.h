@@ -228,6 +228,9 @@ struct LdsCol {
 #ifndef MPCX_DEC_TIGHT
 #define MPCX_DEC_TIGHT 1
 #endif
+#ifndef MPCX_CHAIN_EARLY_EXIT
+#define MPCX_CHAIN_EARLY_EXIT true
+#endif
 #ifndef MPCX_SOFT_INLINE
 #define MPCX_SOFT_INLINE true
 #endif
@@ -1150,6 +1153,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
               }
             }
           }
+          // models with a long chain step (the workspace-stash models, one instance per wave): a
+          // failed inertia test ends the chain early (below)
+          constexpr bool kEarly = MPCX_CHAIN_EARLY_EXIT && kWsStash && !kDec && G == 64;
+          bool early = false;
           // the chain: one step per node, lane j only.  Models without the decoupled suffix take
           // the inertia verdict of their step from its factors after the chain, on all lanes at
           // once (fac_ok), so no lane-mask merge sits on the chain
@@ -1195,9 +1202,19 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
                     Hd, gp, Aop, Bop, cdef, Pin_, pin_, P, p, fac);
               }
             }
+            // a step whose reduced Huu' is not positive definite decides the attempt: the KKT
+            // matrix has the wrong inertia whatever the remaining steps give, so the chain stops
+            // there (one instance per wave, so the verdict is the wave's).  Same decision, same
+            // delta sequence as running the chain out (fac_ok is the test taken after the chain)
+            if constexpr (kEarly) {
+              if (__any(seq && k == j && !fac_ok<NX, NU>(fac))) {
+                early = true;
+                break;
+              }
+            }
           }
           if constexpr (!kDec)
-            if (seq) okl = !hasU || fac_ok<NX, NU>(fac);
+            if (seq) okl = !early && (!hasU || fac_ok<NX, NU>(fac));
         } else {  // wave by wave, N-side first; the value function crosses waves through LDS
           const int wv = (int)(threadIdx.x >> 6);
           for (int ph = XWave<G>::W - 1; ph >= 0; --ph) {
