@@ -194,3 +194,37 @@ def test_bench_group_size_and_usable_cpus():
         else:
             os.environ["OMP_NUM_THREADS"] = old
     assert 1 <= n <= len(os.sched_getaffinity(0)) <= (os.cpu_count() or 1)
+
+
+def test_bench_solve_roofline_uses_only_a_current_pmc_record(tmp_path, monkeypatch):
+    """bench.py's solve-kernel roofline: achieved = algorithmic flops of the launch / its time,
+    frac against the FP64 vector peak; the issued PMC figures and the issue share of wave cycles
+    sit beside it only when the committed record was measured on this tree's sources, and a stale
+    record is named, never used."""
+    import importlib.util
+    import json
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from mpcx import _lib
+
+    kname = "void mpcx::solve_kernel<mpcx::UnicycleFreeModel, 64, false>(mpcx::SolveArgs)"
+    rec = {kname: {"f64_lane_flops_per_group_iteration": 400000.0,
+                   "wave_cycles_share": {"issuing": 0.8, "dependency_or_pipe_stall": 0.02, "waitcnt_or_barrier": 0.18},
+                   "valu_active_share": 0.7}}
+    algo = {"per_iteration": 40000.0, "per_node": {}, "eval_source": "e", "riccati_source": "r"}
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    os.makedirs(tmp_path / os.path.dirname(bench.SOLVE_PMC), exist_ok=True)
+    for current in (True, False):
+        meta = {"mpcx_source_hash": _lib.source_hash() if current else "0000000000000000"}
+        with open(tmp_path / bench.SOLVE_PMC, "w") as f:
+            json.dump({"_meta": meta, **rec}, f)
+        r = bench.solve_roofline("UnicycleFreeModel", 64, algo, 100000, 2.0)  # 4e9 flops in 2 ms
+        assert r["achieved"] == pytest.approx(2.0) and r["frac"] == pytest.approx(2.0 / bench.PEAK_FP64_TFLOPS, abs=1e-5)
+        if current:
+            assert r["issued"]["algorithmic_over_issued"] == pytest.approx(0.1)
+            assert r["issue"]["issuing_share_of_wave_cycles"] == 0.8
+        else:
+            assert isinstance(r["issued"], str) and r["issued"].startswith("stale") and "issue" not in r
