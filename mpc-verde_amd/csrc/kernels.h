@@ -231,6 +231,9 @@ struct LdsCol {
 #ifndef MPCX_CHAIN_EARLY_EXIT
 #define MPCX_CHAIN_EARLY_EXIT true
 #endif
+#ifndef MPCX_DEC_SCAN
+#define MPCX_DEC_SCAN true
+#endif
 #ifndef MPCX_SOFT_INLINE
 #define MPCX_SOFT_INLINE true
 #endif
@@ -257,6 +260,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   __shared__ double sbuf[Model::kParallelRiccati ? RElem<NX>::NE * kSBS : 1];
   // LDS cache of the ODE models' transcendental values across their derivative passes (ode.h)
   __shared__ double tcache[Model::kTrigSlots > 0 ? Model::kTrigSlots * kSBS : 1];
+  // the decoupled suffix's vector scan (multi-wave groups): NX doubles per thread, then the
+  // matrix powers (A^T)^(2^l), l < 8
+  __shared__ double dscan[DecSuffixOf<Model>::value && G > 64 ? NX * kSBS + 8 * NX * NX : 1];
   // workspace chain stash (solver.h chain_ws_slots): slots after the restoration workspace's
   constexpr bool kWsStash = WsStashOf<Model>::value;
   // The stash is one contiguous record per thread (array of structures, after the restoration
@@ -1141,6 +1147,74 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
             jc = __builtin_amdgcn_readfirstlane(jc);  // wave-uniform: scalar loop bounds
           }
         }
+        // The reused suffix as a log-depth scan (multi-wave groups: one instance per block).  On
+        // a reused stage p_k = A^T p_{k+1} + r_k with r_k = gp_x + A^T (P_{k+1} c), and when every
+        // stage of the suffix uses the same table (shared tables) the composition of d steps is
+        // the uniform (A^T)^d: a Hillis-Steele suffix scan v_k += (A^T)^d v_{k+d} carries only the
+        // NX-vector, the powers (A^T)^(2^l) formed once per factorisation by NX^2 threads in LDS.
+        // log2(N) levels replace the suffix's N - jc dependent steps (config 5: 95 of 100).
+        bool sscan = false;  // group-uniform
+        if constexpr (kDec && G > 64 && MPCX_DEC_SCAN) {
+          if (jc < N && !a.lin.per_instance && a.tabseq == nullptr) {
+            const bool mine = k >= jc && k < N;
+            const double ti = (double)((ctx.A - a.lin.A) / (NX * NX));  // my stage's table
+            const double tmax = gmax<G>(mine ? ti : -1.0, xw), tmin = gmin<G>(mine ? ti : 1e300, xw);
+            sscan = tmin == tmax;
+            if (sscan) {
+              const double* Au = a.lin.A + (size_t)tmax * NX * NX;
+              double* mpow = dscan + NX * kSBS;  // level l: (A^T)^(2^l), row-major
+              const int t = (int)threadIdx.x;
+              if (t < NX * NX) mpow[t] = Au[(t % NX) * NX + t / NX];
+              __syncthreads();
+              for (int l = 1; (1 << l) < G && (1 << l) <= N; ++l) {
+                if (t < NX * NX) {
+                  const double* Mp = mpow + (l - 1) * NX * NX;
+                  const int i = t / NX, j = t % NX;
+                  double acc = Mp[i * NX] * Mp[j];
+#pragma unroll
+                  for (int m = 1; m < NX; ++m) acc = fma(Mp[i * NX + m], Mp[m * NX + j], acc);
+                  mpow[l * NX * NX + t] = acc;
+                }
+                __syncthreads();
+              }
+              double v[NX];
+#pragma unroll
+              for (int i = 0; i < NX; ++i) {
+                double acc = gp[i];
+#pragma unroll
+                for (int m = 0; m < NX; ++m)
+                  if (Model::AMASK & (1ull << (m * NX + i))) acc = fma(Aop[m * NX + i], vpc[m], acc);
+                v[i] = mine ? acc : (k == N ? p[i] : 0.0);
+              }
+              for (int d = 1, l = 0; d < G && d <= N; d <<= 1, ++l) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) dscan[i * kSBS + t] = v[i];
+                __syncthreads();
+                if (t + d < G) {
+                  const double* M = mpow + l * NX * NX;
+                  double w[NX];
+#pragma unroll
+                  for (int i = 0; i < NX; ++i) w[i] = dscan[i * kSBS + t + d];
+#pragma unroll
+                  for (int i = 0; i < NX; ++i) {
+                    double acc = v[i];
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) acc = fma(M[i * NX + j], w[j], acc);
+                    v[i] = acc;
+                  }
+                }
+                __syncthreads();
+              }
+              if (seq && mine) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) p[i] = v[i];
+                fac.g0 = gp[NX];
+                if constexpr (NU == 2) fac.g1 = fma(-fac.t, gp[NX], gp[NX + 1]);
+                okl = okd;
+              }
+            }
+          }
+        }
         if constexpr (G <= 64) {
           if constexpr (kDec) {
             for (int j = N - 1; j >= jc; --j) {
@@ -1222,7 +1296,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
               const double* in = xw.prev();  // (P, p) of node 64 (ph + 1), written last phase
               const int jtop = 64 * ph + 63;
               if constexpr (kDec) {  // this wave's reused-suffix steps (see jc above)
-                for (int j = min(N - 1, jtop); j >= max(jc, 64 * ph); --j) {
+                for (int j = min(N - 1, jtop); !sscan && j >= max(jc, 64 * ph); --j) {
                   double pin_[NX];
 #pragma unroll
                   for (int i = 0; i < NX; ++i) pin_[i] = from_next(p[i]);

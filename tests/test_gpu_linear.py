@@ -58,6 +58,11 @@ def X_of(w, nx, nu, N):
     return np.stack(xs, axis=-2)
 
 
+def close(a, b):
+    """max |a - b| relative to max(1, max |b|)"""
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
 def test_pendulum_batch_vs_oracle(mpcx, R, pend):
     lin, S = pend
     from mpcx import lti
@@ -220,8 +225,10 @@ def test_pendulum_long_horizon_multiwave(mpcx, R, N):
     for b in range(B):
         u_ref = R.pendulum_qp_solve(x[b], A, Bd, N=N, uprev=up[b])
         assert rel(r["w"][b, 5:5 + 6 * 5:6], u_ref) <= U_TOL, b
-    # instances are independent: a ragged sub-batch gives bit-identical results
-    r2 = S.solve_batch(lti.pendulum_params(lin, x[5:12], up[5:12]))
+    # instances are independent: a ragged sub-batch gives bit-identical results (a fresh handle:
+    # a second launch of S would start from the suffix cache, whose scan sums in another order)
+    S2 = mpcx.nlpsol("pend", "mi355x", lin, {"ipopt": {"max_iter": 200}})
+    r2 = S2.solve_batch(lti.pendulum_params(lin, x[5:12], up[5:12]))
     np.testing.assert_array_equal(r2["w"], r["w"][5:12])
 
 
@@ -230,7 +237,10 @@ def test_pendulum_decoupled_suffix_same_bits(mpcx, R, N, monkeypatch):
     """The move-blocked stages (B = 0, no x-u cost block) reuse P_k across iterations
     (solver.hip "decoupled suffix", riccati.h DEC), and later launches start from the P_k an
     earlier one cached.  Same solution bits, multipliers and iteration counts as the full
-    recursion (MPCX_DEC_SUFFIX=0), with and without the cache, and the LQ oracle's solution."""
+    recursion (MPCX_DEC_SUFFIX=0), with and without the cache, and the LQ oracle's solution.
+    At N = 100 (two-wave groups) the reused suffix runs as a log-depth vector scan (kernels.h
+    MPCX_DEC_SCAN), whose sums associate differently: there the same iteration counts and a
+    solution within 1e-9 of the full recursion's."""
     from mpcx import lti
 
     lin = lti.inverted_pendulum_qp(N=N)
@@ -251,8 +261,11 @@ def test_pendulum_decoupled_suffix_same_bits(mpcx, R, N, monkeypatch):
     assert np.all(a["status"] == 0)
     for r in (a, a2):
         np.testing.assert_array_equal(r["iters"], b["iters"])
-        np.testing.assert_array_equal(r["w"], b["w"])
-        np.testing.assert_array_equal(r["lam_g"], b["lam_g"])
+        if N < 64:
+            np.testing.assert_array_equal(r["w"], b["w"])
+            np.testing.assert_array_equal(r["lam_g"], b["lam_g"])
+        else:
+            assert close(r["w"], b["w"]) <= 1e-9 and close(r["lam_g"], b["lam_g"]) <= 1e-9
     A, Bd = R.pendulum_model()
     for i in range(0, B, 7):
         u_ref = R.pendulum_qp_solve(x[i], A, Bd, N=N, uprev=up[i])
@@ -380,7 +393,10 @@ def test_pendulum_run_equals_lockstep_decoupled_suffix(mpcx, dec, monkeypatch):
     """The config-5 path as benchmarked: DeviceLoop.run(K) (one multi-step launch: warm duals,
     mu_init 1e-4, kb / pcv re-derived at every step boundary, two-wave groups at N = 100) against
     K lock-step launches, with the decoupled-suffix reuse on and off (MPCX_DEC_SUFFIX=0): the same
-    bits for w, multipliers, iterations and status at every step."""
+    iterations and status at every step, and the same bits for w and the multipliers with the
+    reuse off; with it on, within 1e-9 (lock-step launches after the first start from the suffix
+    cache and take the vector scan at their first factorisation, where the steps of a multi-step
+    launch run the full recursion first; the two sum in different orders)."""
     import torch
     from mpcx import dist as mdist
     from mpcx import lti
@@ -403,14 +419,21 @@ def test_pendulum_run_equals_lockstep_decoupled_suffix(mpcx, dec, monkeypatch):
     np.testing.assert_array_equal(it_r.cpu().numpy(), np.array(it_l))
     assert np.all(np.array(st_l) == 0)
     for n in ("P", "w", "w0", "lam", "lamx", "f"):
-        np.testing.assert_array_equal(getattr(run, n).cpu().numpy(), getattr(lock, n).cpu().numpy(), err_msg=n)
+        got, want = getattr(run, n).cpu().numpy(), getattr(lock, n).cpu().numpy()
+        if dec == "0":
+            np.testing.assert_array_equal(got, want, err_msg=n)
+        else:
+            assert close(got, want) <= 1e-9, n
 
 
 def test_pendulum_suffix_cache_follows_table_changes(mpcx):
     """The decoupled suffix's P_k cached across launches (capi SolveArgs::pcache) belong to one
     table generation: after mpcx_set_linear_model with other weights (q), and after a schedule
     change that moves the free/blocked boundary (n_free), a handle that has cached the old
-    suffix gives the same bits as a fresh handle of the new problem."""
+    suffix gives the same result as a fresh handle of the new problem: the same iteration counts
+    and a solution within 1e-9 (not the same bits: the cached handle's first factorisation
+    already takes the suffix scan, the fresh handle's runs the full recursion; a stale cache
+    would give another problem's solution)."""
     from mpcx import lti
 
     N, B = 100, 64
@@ -424,7 +447,8 @@ def test_pendulum_suffix_cache_follows_table_changes(mpcx):
     for _ in range(2):  # fill, then use, the cache of lin1
         r1 = S.solve_batch(P)
     ref1 = mpcx.nlpsol("pc1", "mi355x", lin1, {"ipopt": {"max_iter": 200}}).solve_batch(P)
-    np.testing.assert_array_equal(r1["w"], ref1["w"])
+    np.testing.assert_array_equal(r1["iters"], ref1["iters"])
+    assert close(r1["w"], ref1["w"]) <= 1e-9
     for lin in (lin2, lin3):
         S.set_linear_model(lin)
         r = S.solve_batch(P)
@@ -432,7 +456,7 @@ def test_pendulum_suffix_cache_follows_table_changes(mpcx):
         ref = mpcx.nlpsol("pcf", "mi355x", lin, {"ipopt": {"max_iter": 200}}).solve_batch(P)
         assert np.all(ref["status"] == 0)
         for got in (r, r_again):
-            np.testing.assert_array_equal(got["w"], ref["w"])
+            assert close(got["w"], ref["w"]) <= 1e-9
             np.testing.assert_array_equal(got["iters"], ref["iters"])
         assert np.max(np.abs(r["w"] - r1["w"])) > 1e-6  # the problems really differ
 
