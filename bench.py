@@ -99,7 +99,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--group-policy", type=int, default=0, choices=(0, 1),
                     help="mpcx_spec.group_policy: 0 widens lane groups to fill the SIMDs, 1 keeps the smallest")
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5),
@@ -118,6 +118,8 @@ def parse():
     ap.add_argument("--roofline-reps", type=int, default=20)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-reference-warm-start", action="store_true",
+                    help="skip the second timing under the reference's warm start (shifted primal only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum timed CPU-baseline solve time")
     ap.add_argument("--profile-sweep-only", action="store_true", help="only launch the sweep (for rocprofv3 --pmc)")
     return ap.parse_args()
@@ -148,11 +150,25 @@ def shift_lamx_np(lamx, N):
     return out
 
 
+REF_IPOPT = {"max_iter": 2000, "acceptable_tol": 1e-8, "acceptable_obj_change_tol": 1e-6}  # :188-196
+# warm-start policies of the closed loop (the solve after a shift):
+#   "dual": shifted primal AND multipliers, IPOPT warm_start_init_point (mu0 = bound push =
+#           multiplier push = 1e-4, mpcx_spec.warm_*) -- a solver option the reference does not set;
+#   "reference": the reference's own -- the shifted primal guess only, IPOPT's default start
+#           (mu0 = 0.1, multipliers 0 / 1): Casadi/multiple_shooting_casadi.py:233-242,274-287
+#           (args['x0'] = w0, no lam_x0 / lam_g0), in the interleaved layout
+POLICY = {"dual": "warm start: shifted primal + shifted multipliers, IPOPT warm_start_init_point (mu0 1e-4)",
+          "reference": "warm start as the reference: shifted primal only, IPOPT default initialisation "
+                       "(mu0 0.1; multiple_shooting_casadi.py:233-242,274-287)"}
+
+
 def cpu_baseline(make_P, N, steps, cores, min_seconds=10.0, max_reps=64, warm=(1e-4, 1e-4, 1e-4)):
-    """C++ oracle (port of the same NLP + IPOPT-style IPM) on host cores: closed loops of
-    `steps` steps with the same warm start as the GPU loop (first step cold, then shifted
-    primal + multipliers), solve calls timed.  Repeated on fresh instance blocks
-    (make_P(rep) -> (B, 6)) until >= min_seconds of solve time (a bounded sample)."""
+    """C++ oracle (port of the same NLP + IPOPT-style IPM, the reference's IPOPT options) on host
+    cores: closed loops of `steps` steps with the GPU loop's warm-start policy (first step cold,
+    then the shifted primal plus -- warm given -- the shifted multipliers as IPOPT's
+    warm_start_init_point; warm=None: the shifted primal only, the reference's policy), solve
+    calls timed.  Repeated on fresh instance blocks (make_P(rep) -> (B, 6)) until >= min_seconds
+    of solve time (a bounded sample).  Returns (solves/s, seconds, reps, mean iterations)."""
     from oracle import ipm_ref, nlp_ref
 
     ipm_ref.build()
@@ -160,6 +176,7 @@ def cpu_baseline(make_P, N, steps, cores, min_seconds=10.0, max_reps=64, warm=(1
     t_solve = 0.0
     n = 0
     reps = 0
+    its = 0
     while reps < max_reps and (reps == 0 or t_solve < min_seconds):
         P = make_P(reps).copy()
         B = P.shape[0]
@@ -167,21 +184,20 @@ def cpu_baseline(make_P, N, steps, cores, min_seconds=10.0, max_reps=64, warm=(1
         lam0 = lamx0 = None
         for s in range(steps):
             t0 = time.perf_counter()
-            if s == 0:
-                r = ipm_ref.solve_batch(ocp, P, w0=w0, nthreads=cores)
-                r["lam_x"] = np.zeros_like(r["w"])
+            if s == 0 or warm is None:
+                r = ipm_ref.solve(ocp, P, w0=w0, nthreads=cores, **REF_IPOPT)
             else:
-                r = ipm_ref.solve_batch_warm(ocp, P, w0, lam0=lam0, lamx0=lamx0, mu_init=warm[0],
-                                             bound_push=warm[1], mult_push=warm[2], nthreads=cores)
+                r = ipm_ref.solve(ocp, P, w0=w0, lam0=lam0, lamx0=lamx0, warm=warm, nthreads=cores, **REF_IPOPT)
             t_solve += time.perf_counter() - t0
             n += B
+            its += int(r["iters"].sum())
             xf, _ = nlp_ref.F(P[:, 0:3], r["w"][:, 3:5], P[:, 3:6], ocp)
             P[:, 0:3] = xf
             w0 = shift_np(r["w"], N)
             lam0 = shift_lam_np(r["lam_g"], N)
             lamx0 = shift_lamx_np(r["lam_x"], N)
         reps += 1
-    return n / t_solve, t_solve, reps
+    return n / t_solve, t_solve, reps, its / max(n, 1)
 
 
 def _pseq(refs, n_p, nx):
@@ -440,8 +456,9 @@ def main():
 
     import torch
 
-    # every rank check happens before the first GPU call (device_count does not initialise HIP)
-    plan, argv = launch_plan(args.gpus, n_devices=torch.cuda.device_count())
+    # the launch plan is decided before any GPU call, on a device count read from the KFD
+    # topology (mdist.visible_gpu_count never initialises HIP)
+    plan, argv = launch_plan(args.gpus, n_devices=mdist.visible_gpu_count())
     if plan == "spawn":
         import subprocess
 
@@ -451,6 +468,8 @@ def main():
     assert world == args.gpus
 
     local = mdist.device_index(local)
+    if local >= torch.cuda.device_count():  # each rank checks its own GPU (this rank's first GPU call)
+        raise SystemExit(f"rank {rank}: GPU {local} not visible ({torch.cuda.device_count()} device(s))")
     torch.cuda.set_device(local)
     mdist.init(mdist.backend("nccl"))
     import mpcx
@@ -529,81 +548,104 @@ def main():
         seq = lambda t0, K: (_pseq(refs[t0:t0 + K], P0.shape[1], 4), tabs[t0:t0 + K].contiguous())  # noqa: E731
     else:
         P0 = mpcx.lti.pendulum_params(ocp, mdist.config5_inputs(start, stop), 0.0)
-    loop = DeviceLoop(solver, P0, device=dev, stream=stream)
-
-    warm_it = torch.zeros((max(args.warmup, 1), B), dtype=torch.int32, device=loop.P.device)
-    for t in range(args.warmup):
-        if per_step is not None:
-            per_step(loop, t)
-        loop.step(iters_out=warm_it[t])
-    torch.cuda.synchronize()
     K = args.steps
-    iters_hist = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
-    status_hist = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
-    t_seq = args.warmup
-    if per_step is not None:
-        per_step(loop, t_seq)  # current references / schedule = those of the first timed step
-    Pseq, tabseq = seq(t_seq, K)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev_run = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-    if args.mode == "async":
-        # K closed-loop steps in ONE launch; every instance runs its own receding-horizon loop
-        # (bit-identical to K lock-step launches, tests/test_gpu_parity.py::test_run_*)
-        ev_run[0].record(stream)
-        loop.run(K, status_out=status_hist, iters_out=iters_hist, Pseq=Pseq, tabseq=tabseq)
-        ev_run[1].record(stream)
-    else:
-        for i in range(K):
-            if per_step is not None and i > 0:
-                per_step(loop, t_seq + i)
-            loop.step(status_out=status_hist[i], iters_out=iters_hist[i])
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = mdist.max_over_ranks(t1 - t0, device=loop.P.device)
 
-    # lock-step latency: K further steps, one launch each, HIP events on the launch stream
-    # (ms_per_solve_p50 = the latency a real-time loop sees per closed-loop step)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    lk_st = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
-    lk_it = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
-    torch.cuda.synchronize()
-    tl0 = time.perf_counter()
-    for i in range(K):
+    def closed_loop(warm_duals):
+        """W untimed warm-up steps, K timed steps (one multi-step launch, or K launches in
+        --mode lockstep), then K lock-step launches timed with HIP events (the latency a real-time
+        loop sees per step), under one warm-start policy (POLICY).  Every policy starts from the
+        same P0 and the same per-step references."""
+        loop = DeviceLoop(solver, P0, device=dev, stream=stream, warm_duals=warm_duals)
+        warm_it = torch.zeros((max(args.warmup, 1), B), dtype=torch.int32, device=loop.P.device)
+        for t in range(args.warmup):
+            if per_step is not None:
+                per_step(loop, t)
+            loop.step(iters_out=warm_it[t])
+        torch.cuda.synchronize()
+        iters_hist = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
+        status_hist = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
+        t_seq = args.warmup
         if per_step is not None:
-            per_step(loop, args.warmup + K + i)
-        ev[i][0].record(stream)
-        loop.step(status_out=lk_st[i], iters_out=lk_it[i])
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    tl1 = time.perf_counter()
-    lock_elapsed = mdist.max_over_ranks(tl1 - tl0, device=loop.P.device)
-    solve_ms = sorted(a.elapsed_time(b) for a, b in ev)
-    p50 = mdist.max_over_ranks(float(np.median(solve_ms)), device=loop.P.device)
-    lock_iters_max = mdist.max_over_ranks(float(lk_it.max(dim=1).values.double().mean().item()), device=loop.P.device)
+            per_step(loop, t_seq)  # current references / schedule = those of the first timed step
+        Pseq, tabseq = seq(t_seq, K)
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev_run = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        if args.mode == "async":
+            # K closed-loop steps in ONE launch; every instance runs its own receding-horizon loop
+            # (bit-identical to K lock-step launches, tests/test_gpu_parity.py::test_run_*)
+            ev_run[0].record(stream)
+            loop.run(K, status_out=status_hist, iters_out=iters_hist, Pseq=Pseq, tabseq=tabseq)
+            ev_run[1].record(stream)
+        else:
+            for i in range(K):
+                if per_step is not None and i > 0:
+                    per_step(loop, t_seq + i)
+                loop.step(status_out=status_hist[i], iters_out=iters_hist[i])
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if world > 1:
+            torch.distributed.barrier()
+        elapsed = mdist.max_over_ranks(t1 - t0, device=loop.P.device)
+
+        # lock-step latency: K further steps, one launch each, HIP events on the launch stream
+        # (ms_per_solve_p50 = the latency a real-time loop sees per closed-loop step)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        lk_st = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
+        lk_it = torch.zeros((K, B), dtype=torch.int32, device=loop.P.device)
+        torch.cuda.synchronize()
+        tl0 = time.perf_counter()
+        for i in range(K):
+            if per_step is not None:
+                per_step(loop, args.warmup + K + i)
+            ev[i][0].record(stream)
+            loop.step(status_out=lk_st[i], iters_out=lk_it[i])
+            ev[i][1].record(stream)
+        torch.cuda.synchronize()
+        tl1 = time.perf_counter()
+        lock_elapsed = mdist.max_over_ranks(tl1 - tl0, device=loop.P.device)
+        solve_ms = sorted(a.elapsed_time(b) for a, b in ev)
+        dv = loop.P.device
+        return {"loop": loop, "warm_it": warm_it, "iters_hist": iters_hist, "status_hist": status_hist,
+                "lk_st": lk_st, "lk_it": lk_it, "elapsed": elapsed, "lock_elapsed": lock_elapsed,
+                "solve_ms": solve_ms, "p50": mdist.max_over_ranks(float(np.median(solve_ms)), device=dv),
+                "lock_iters_max": mdist.max_over_ranks(float(lk_it.max(dim=1).values.double().mean().item()), device=dv),
+                "iters_max_step": mdist.max_over_ranks(float(iters_hist.max(dim=1).values.double().mean().item()),
+                                                       device=dv),
+                "iters_mean": mdist.max_over_ranks(float(iters_hist.double().mean().item()), device=dv),
+                "run_ms": ev_run[0].elapsed_time(ev_run[1]) if args.mode == "async" else float(np.sum(solve_ms))}
+
+    res = closed_loop(warm_duals=True)  # the headline policy ("dual")
+    ref_res = closed_loop(warm_duals=False) if not args.no_reference_warm_start else None
+    loop, warm_it, iters_hist, status_hist = res["loop"], res["warm_it"], res["iters_hist"], res["status_hist"]
+    lk_it, elapsed, lock_elapsed, solve_ms = res["lk_it"], res["elapsed"], res["lock_elapsed"], res["solve_ms"]
+    p50, lock_iters_max = res["p50"], res["lock_iters_max"]
 
     # closed-loop statistics: the only collective (RCCL all_gather over xGMI), outside the timed region
-    P_fin = loop.P.cpu().numpy()
-    if variant is not None:  # first three states against the stage-0 reference / set point
-        P_fin = np.concatenate([P_fin[:, 0:3], P_fin[:, ocp.nx:ocp.nx + 3]], axis=1)
-    elif cfg == 3:  # final error against the stage-0 reference
-        P_fin = np.concatenate([P_fin[:, 0:3], P_fin[:, 3:6]], axis=1)
-    elif cfg == 4:  # (y, phi, v_y) against the stage-0 reference
-        P_fin = np.concatenate([P_fin[:, 0:3], P_fin[:, 4:7]], axis=1)
-    elif cfg == 5:  # (x, x', th) against the set point (10, 0, 0)
-        P_fin = np.concatenate([P_fin[:, 0:3], np.tile([ocp.x_target, 0.0, 0.0], (B, 1))], axis=1)
-    S = mdist.stats_matrix(P_fin, None, loop.f.cpu().numpy(), status_hist.max(dim=0).values.cpu().numpy(),
+    def P_fin_of(lp):
+        """Final state next to its target (first three states) for the stats matrix."""
+        Pf = lp.P.cpu().numpy()
+        if variant is not None:  # first three states against the stage-0 reference / set point
+            return np.concatenate([Pf[:, 0:3], Pf[:, ocp.nx:ocp.nx + 3]], axis=1)
+        if cfg == 3:  # final error against the stage-0 reference
+            return np.concatenate([Pf[:, 0:3], Pf[:, 3:6]], axis=1)
+        if cfg == 4:  # (y, phi, v_y) against the stage-0 reference
+            return np.concatenate([Pf[:, 0:3], Pf[:, 4:7]], axis=1)
+        if cfg == 5:  # (x, x', th) against the set point (10, 0, 0)
+            return np.concatenate([Pf[:, 0:3], np.tile([ocp.x_target, 0.0, 0.0], (B, 1))], axis=1)
+        return Pf
+
+    S = mdist.stats_matrix(P_fin_of(loop), None, loop.f.cpu().numpy(), status_hist.max(dim=0).values.cpu().numpy(),
                            iters_hist.cpu().numpy())
     S_all = mdist.all_gather_stats(S, device=loop.P.device)
-    iters_max_step = mdist.max_over_ranks(float(iters_hist.max(dim=1).values.double().mean().item()),
-                                          device=loop.P.device)
+    iters_max_step = res["iters_max_step"]
 
-    # group-iterations of every solve launch of this run (PMC normalisation, tools/solve_pmc_summary.py)
-    iters_all = int(warm_it[:args.warmup].sum().item() + iters_hist.sum().item() + lk_it.sum().item())
+    # group-iterations of every solve launch of this run, both policies (PMC normalisation,
+    # tools/solve_pmc_summary.py)
+    iters_all = sum(int(r["warm_it"][:args.warmup].sum().item() + r["iters_hist"].sum().item() +
+                        r["lk_it"].sum().item()) for r in (res, ref_res) if r is not None)
 
     roof = None
     if rank == 0 and not args.no_roofline and cfg == 2:
@@ -621,10 +663,8 @@ def main():
     # events on the launch stream) or the mean single-step launch (lock-step latency run)
     n_simd = 4 * torch.cuda.get_device_properties(local).multi_processor_count
     G = group_size(N, B, n_simd, solver.group_policy)
-    if args.mode == "async":
-        run_ms, run_iters = ev_run[0].elapsed_time(ev_run[1]), int(iters_hist.sum().item())
-    else:
-        run_ms, run_iters = float(np.sum(solve_ms)), int(lk_it.sum().item())
+    run_ms = res["run_ms"]
+    run_iters = int(iters_hist.sum().item()) if args.mode == "async" else int(lk_it.sum().item())
     kname = VARIANT_KERNEL[variant] if variant else CFG_KERNEL[cfg]
     algo, why_not = algorithmic_flops_per_iteration(variant or cfg, ocp, N)
     roof_solve = solve_roofline(kname, G, algo, run_iters, run_ms) if rank == 0 else None
@@ -634,20 +674,28 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and cfg == 2:
         cores = usable_cpus()
+        steps = args.warmup + args.steps
         make_P = lambda r: mdist.config2_inputs(r * B, (r + 1) * B, args.seed)  # noqa: E731
-        rate, t, reps = cpu_baseline(make_P, N, args.warmup + args.steps, cores, min_seconds=args.cpu_seconds)
+        rate, t, reps, its = cpu_baseline(make_P, N, steps, cores, min_seconds=args.cpu_seconds)
         # the reference's own loop is one solve at a time on one core (multiple_shooting_casadi.py:226-298)
         B1 = 128
-        rate1, t1, reps1 = cpu_baseline(lambda r: make_P(r)[:B1], N, args.warmup + args.steps, 1,
-                                        min_seconds=args.cpu_seconds / 2)
+        rate1, t1, reps1, _ = cpu_baseline(lambda r: make_P(r)[:B1], N, steps, 1, min_seconds=args.cpu_seconds / 2)
         cpu = {"value": round(rate, 1), "unit": "solves/s", "cores": cores, "kind": "port",
-               "sample": f"{reps} x ({args.warmup + args.steps}-step closed loop of {B} config-2 instances, "
-                         f"N={N}, same warm start as the GPU loop); {t:.1f} s of timed solve calls on {cores} "
-                         "OpenMP threads",
+               "policy": POLICY["dual"],
+               "sample": f"{reps} x ({steps}-step closed loop of {B} config-2 instances, N={N}, the GPU loop's "
+                         f"warm start and IPOPT options); {t:.1f} s of timed solve calls on {cores} OpenMP threads",
+               "iters_mean": round(its, 2),
                "value_1core": round(rate1, 1),
-               "sample_1core": f"{reps1} x ({args.warmup + args.steps}-step closed loop of {B1} instances), "
-                               f"{t1:.1f} s on 1 thread",
+               "sample_1core": f"{reps1} x ({steps}-step closed loop of {B1} instances), {t1:.1f} s on 1 thread",
                "host_cpus": os.cpu_count(), "usable_cpus": cores, "cpu_model": cpu_model()}
+        if ref_res is not None:  # the same loops under the reference's warm start (shifted primal only)
+            rate_r, t_r, reps_r, its_r = cpu_baseline(make_P, N, steps, cores, min_seconds=args.cpu_seconds,
+                                                      warm=None)
+            cpu["reference_warm_start"] = {
+                "value": round(rate_r, 1), "unit": "solves/s", "cores": cores, "policy": POLICY["reference"],
+                "iters_mean": round(its_r, 2),
+                "sample": f"{reps_r} x ({steps}-step closed loop of {B} config-2 instances), {t_r:.1f} s of timed "
+                          f"solve calls on {cores} OpenMP threads"}
 
     # the kernel that dominates the timed step: the fused solve (+ plant/shift) launch.  Its HBM
     # traffic is its inputs and outputs only, so neither HBM nor the FP64 pipes bound it: it is
@@ -662,6 +710,29 @@ def main():
                   "hbm_bytes_per_launch": io_bytes,
                   "hbm_frac": round(io_bytes / (p50 * 1e-3) / 1e9 / PEAK_HBM_GBS, 5)}
     solve_info.update({"group_size": G, "timed_launch_ms": round(run_ms, 4), "timed_group_iterations": run_iters})
+    ref_block = None
+    if ref_res is not None:
+        # the same K-step / lock-step timing with the reference's warm start (POLICY["reference"]);
+        # value / lockstep.value / ms_per_solve_p50 / iters as for the headline policy above
+        r_ = ref_res
+        S_r = mdist.all_gather_stats(mdist.stats_matrix(P_fin_of(r_["loop"]), None, r_["loop"].f.cpu().numpy(),
+                                                        r_["status_hist"].max(dim=0).values.cpu().numpy(),
+                                                        r_["iters_hist"].cpu().numpy()), device=loop.P.device)
+        ref_block = {
+            "value": round(world * B * K / r_["elapsed"], 1), "unit": "solves/s",
+            "ms_per_step": round(r_["elapsed"] / K * 1e3, 4),
+            "lockstep": {"value": round(world * B * K / r_["lock_elapsed"], 1),
+                         "ms_per_step": round(r_["lock_elapsed"] / K * 1e3, 4),
+                         "iters_max_per_step_mean": round(float(r_["lock_iters_max"]), 2)},
+            "ms_per_solve_p50": round(r_["p50"], 4),
+            "workload": (workload_name_v(variant, N, ocp.M) if variant else workload_name(cfg, N)) + "; " +
+                        POLICY["reference"],
+            "warm_start_policy": "reference",
+            "iters_mean": round(float(S_r[:, 1].mean()), 2), "iters_max": int(S_r[:, 2].max()),
+            "iters_max_per_step_mean": round(float(r_["iters_max_step"]), 2),
+            "failed_instances": int((S_r[:, 3] > 1).sum()),
+            "us_per_ipm_iteration": round(r_["p50"] * 1e3 / max(r_["lock_iters_max"], 1.0), 2),
+            "timed_launch_ms": round(r_["run_ms"], 4)}
     if rank == 0:
         total = world * B * K
         out = {
@@ -674,7 +745,9 @@ def main():
             "ms_per_solve_p50": round(p50, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64",
             "data": DATA_V[variant] if variant else DATA[cfg],
-            "config": {"workload": workload_name_v(variant, N, ocp.M) if variant else workload_name(cfg, N),
+            "config": {"workload": (workload_name_v(variant, N, ocp.M) if variant else workload_name(cfg, N)) +
+                                   "; " + POLICY["dual"],
+                       "warm_start_policy": "dual",
                        "dynamics": DYN_V[variant] if variant else DYN[cfg], "N": N,
                        "M": getattr(ocp, "M", None), "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"instance-sharded x{world} (no data-path collective)"},
@@ -682,6 +755,7 @@ def main():
             "iters_max_per_step_mean": round(float(iters_max_step), 2),
             "failed_instances": int((S_all[:, 3] > 1).sum()),
             "iters_sum_all_steps": int(iters_all),
+            "reference_warm_start": ref_block,
             "roofline": roof_solve, "roofline_sweep": roof, "cpu_baseline": cpu, "solve_kernel": solve_info,
             "mpcx_source_hash": _lib.source_hash(),
         }

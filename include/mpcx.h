@@ -120,9 +120,10 @@ typedef struct mpcx_spec {
      Casadi/multiple_shooting_casadi.py:188-196).  A field left 0 takes IPOPT's default:
      dual_inf_tol 1, constr_viol_tol 1e-4, compl_inf_tol 1e-4 (unscaled tests next to tol),
      acceptable_tol 1e-6, acceptable_dual_inf_tol 1e10, acceptable_constr_viol_tol 1e-2,
-     acceptable_compl_inf_tol 1e-2, acceptable_iter 15 (-1 disables the acceptable-level
-     termination).  acceptable_obj_change_tol is taken literally (IPOPT accepts 0); a NEGATIVE
-     value selects IPOPT's default 1e20.  mpcx_default_spec fills every field: the unicycle gets
+     acceptable_compl_inf_tol 1e-2, acceptable_obj_change_tol 1e20, acceptable_iter 15 (-1
+     disables the acceptable-level termination).  IPOPT's literal acceptable_obj_change_tol = 0
+     is expressed as the smallest positive double (4.9e-324, the same test); a negative value
+     also selects the default.  mpcx_default_spec fills every field: the unicycle gets
      the reference script's acceptable_tol 1e-8 / acceptable_obj_change_tol 1e-6 (the problem of
      :181-197 as the script builds it), the ODE models IPOPT's defaults.  (mpcx.nlpsol without
      options uses IPOPT's defaults for every model, as ca.nlpsol without options does.) */
@@ -155,7 +156,13 @@ const char* mpcx_source_hash(void);
  *   W n_tab x nz(nz+1)/2 packed upper triangle of the stage weight (nz = nx+nu),
  *   tab tab_rows x N int32 table index of each stage; tab_rows = 1 (shared by all
  *   instances) or >= the batch size (row b = instance b; LTV schedules).
- * Call before solving; may be called again (e.g. per closed-loop step). */
+ * Call before solving; may be called again (e.g. per closed-loop step).
+ * Reproducibility: with shared tables whose stages end in a decoupled suffix (B = 0, no x-u
+ * weight; the move-blocked cart-pole QP), a launch that finds the suffix's value functions
+ * cached by an earlier launch of this handle sums the suffix's linear part as a log-depth scan,
+ * a fresh handle's first factorisation in chain order: the same solve then agrees to rounding
+ * (~1e-12 relative) and in iteration counts, not bit for bit, across the two cache states.
+ * Launches in the same cache state are bit-identical. */
 int mpcx_set_linear_model(mpcx_handle* h, int32_t n_tab, const double* A, const double* B, const double* c,
                           const double* W, const int32_t* tab, int32_t tab_rows);
 
@@ -181,7 +188,10 @@ int mpcx_dims(const mpcx_handle* h, int32_t* n_w, int32_t* n_g, int32_t* n_p);
  *          default (mu = 0.1, multipliers 0 / 1).
  *   lbw/ubw n_w bound vectors shared by the batch, or NULL = spec bounds
  *          (the reference's lbx/ubx, :199-206; X_0 is always free: it is
- *          pinned by the lifted constraint g_0)
+ *          pinned by the lifted constraint g_0 = x0 - X_0 and enters nothing else --
+ *          interval 0 integrates from the parameter x0, F(x0=[P[:nx]; ...], p=U_0),
+ *          as the script does at :125,157, so lam_g[0:nx] is 0 at a solution: exactly
+ *          from a start without multipliers, to the dual tolerance from a warm one)
  *   w_out  B x n_w optimal decision vectors (interleaved reference layout)
  *   f_out  B objective values, or NULL
  *   g_out  B x n_g constraint values at w_out, or NULL

@@ -523,8 +523,8 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
     a.acc_dual_inf_tol = d(sp.acceptable_dual_inf_tol, 1e10);
     a.acc_constr_viol_tol = d(sp.acceptable_constr_viol_tol, 1e-2);
     a.acc_compl_inf_tol = d(sp.acceptable_compl_inf_tol, 1e-2);
-    // taken literally (0 included); negative = IPOPT's default
-    a.acc_obj_change_tol = sp.acceptable_obj_change_tol < 0 ? 1e20 : sp.acceptable_obj_change_tol;
+    // 0 (a zero-filled spec) or negative = IPOPT's default, as for every field above
+    a.acc_obj_change_tol = d(sp.acceptable_obj_change_tol, 1e20);
     a.acc_iter = sp.acceptable_iter == 0 ? 15 : (sp.acceptable_iter < 0 ? 0 : sp.acceptable_iter);
     a.restoration = sp.no_restoration ? 0 : 1;
   }

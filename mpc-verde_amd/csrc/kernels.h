@@ -431,9 +431,22 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 
   // ---- stage evaluation (all lanes evaluate -- SIMD, no extra cost -- lanes without an
   //      interval mask the results; A and B keep their structural constants)
+  //      Interval 0 integrates from the parameter x0, not from X_0 (the script's
+  //      Xk = P[:n_states], F(x0=vertcat(Xk, P[3:]), p=U_0): multiple_shooting_casadi.py:125,157),
+  //      so the lifted X_0 enters only g_0 = x0 - X_0: lane 0's A_0, its x-gradient and its x
+  //      Hessian blocks are zero in the NLP.  Lane 0 evaluates at (x0, U_0), its x-gradient is
+  //      masked here, and the Newton step treats A_0 as zero (K_0 = 0, P_0 = Sigma_x + delta,
+  //      p_0 = the barrier gradient, dx_1 independent of dx_0: riccati / forward below).
   double xf[NX], qv, A[NX * NX], Bm[NX * NU], gq[NZ], Hs[NH];
   double cdef[NX], c0[NX];  // cdef = F(X_k,U_k) - X_{k+1} (constraint k+1), c0 = x0 - X_0 (lane 0)
   double fs = 1.0;
+  // the stage's evaluation point: (x0, U_0) on lane 0, (X_k, U_k) elsewhere
+  auto stage_point = [&](const double* zz, double* ze) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i) ze[i] = (k == 0) ? x0[i] : zz[i];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) ze[NX + i] = zz[NX + i];
+  };
   // evaluation at the point (zz, ll): also the line search's first trial when the model's
   // kEvalInSearch is set
   auto eval_at = [&](const double* zz, const double* ll) __attribute__((always_inline)) {
@@ -449,14 +462,16 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       ln[i] = nxt[i];
       xn[i] = nxt[NX + i];
     }
-    Model::derivs(ma, ctx, zz, ln, fs, xf, qv, A, Bm, gq, Hs);
-    const double m = hasU ? 1.0 : 0.0;
+    double ze[NZ];
+    stage_point(zz, ze);
+    Model::derivs(ma, ctx, ze, ln, fs, xf, qv, A, Bm, gq, Hs);
+    const double m = hasU ? 1.0 : 0.0, mx = (hasU && k > 0) ? 1.0 : 0.0;  // no x-gradient at X_0
     qv *= m;
     if constexpr (!Model::kTableHess)
 #pragma unroll
       for (int i = 0; i < NH; ++i) Hs[i] *= m;
 #pragma unroll
-    for (int i = 0; i < NZ; ++i) gq[i] *= m;
+    for (int i = 0; i < NZ; ++i) gq[i] *= (i < NX) ? mx : m;
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
       cdef[i] = hasU ? xf[i] - xn[i] : 0.0;
@@ -490,6 +505,11 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   // line search.
   constexpr bool kRes = RestoOf<Model>::value;
   const bool res_on = kRes && a.restoration != 0;  // kernel-uniform
+  // The solve launch clears every thread's park slot first, so the resume launch that follows
+  // sees exactly the instances THIS launch parked: the workspace is laid out by this launch's
+  // thread count, and an earlier launch at another batch size may have left slots set there
+  if constexpr (kRes && !RESUME)
+    if (a.ws) a.ws[(long)(RestoWs::SC(NX, NZ) + RestoWs::sPEND) * a.ws_stride + gid] = 0.0;
   // Models whose line search evaluates derivatives at its first trial (the unicycle) take IPOPT's
   // soft restoration step in the solve loop (a cold block after the line search).  Only the
   // restoration phase proper parks the instance for the resume launch, so an instance whose line
@@ -826,11 +846,12 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
       for (int i = 0; i < NX; ++i) rd[i] = gq[i] - lam[i];
       if (hasU) {
+        if (k > 0)  // (X_0 enters only g_0)
 #pragma unroll
-        for (int j = 0; j < NX; ++j)
+          for (int j = 0; j < NX; ++j)
 #pragma unroll
-          for (int m = 0; m < NX; ++m)
-            if (Model::AMASK & (1ull << (m * NX + j))) rd[j] = fma(Model::jacA(ctx, A)[m * NX + j], ln[m], rd[j]);
+            for (int m = 0; m < NX; ++m)
+              if (Model::AMASK & (1ull << (m * NX + j))) rd[j] = fma(Model::jacA(ctx, A)[m * NX + j], ln[m], rd[j]);
 #pragma unroll
         for (int l = 0; l < NU; ++l) {
           double acc = gq[NX + l];
@@ -1347,6 +1368,17 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         }
       }
       stash(true);
+      // node 0: A_0 = 0 and no x blocks in stage 0 (interval 0 integrates from x0), so the step
+      // gives P_0 = Sigma_x + delta and p_0 = the barrier gradient, as at node N; its factors
+      // (Huu', gu', the inertia test) do not involve A_0 and stand as computed
+      if (k == 0) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+#pragma unroll
+          for (int j = i; j < NX; ++j) P[symix(i, j, NX)] = (i == j) ? sgv[i] + delta : 0.0;
+          p[i] = gp[i];
+        }
+      }
 #pragma unroll
       for (int i = 0; i < NP; ++i) Pk[i] = P[i];
 #pragma unroll
@@ -1393,6 +1425,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       }
     }
     riccati_gains<NX, NU>(fac, Kk, kfk);  // all lanes at once
+    if (k == 0)  // Hux'_0 = 0 (A_0 = 0): no feedback on X_0
+#pragma unroll
+      for (int i = 0; i < NU * NX; ++i) Kk[i] = 0.0;
 
     STAMP(4);
     phase();
@@ -1460,8 +1495,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
               for (int i = 0; i < NM; ++i) prv[i] = xw.prev()[(wv - 1) * kXchStride + i];
           }
+          // lane 1 takes only T_0's constant part: dx_1 = B_0 du_0 + c_1 does not depend on dx_0
+          // (interval 0 integrates from x0, A_0 = 0)
 #pragma unroll
-          for (int i = 0; i < NX * NX; ++i) Am[i] = (k == 0) ? 0.0 : prv[i];
+          for (int i = 0; i < NX * NX; ++i) Am[i] = (k <= 1) ? 0.0 : prv[i];
 #pragma unroll
           for (int i = 0; i < NX; ++i) cm[i] = (k == 0) ? c0v_[i] : prv[NX * NX + i];
         }
@@ -1638,8 +1675,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       } else {
         double xtn[NX];
         group_next<G, NX>(zt, xtn, xw);
-        double xft[NX], qt;
-        Model::value(ma, ctx, zt, xft, qt);
+        double xft[NX], qt, ze[NZ];
+        stage_point(zt, ze);
+        Model::value(ma, ctx, ze, xft, qt);
         if (hasU) {
 #pragma unroll
           for (int i = 0; i < NX; ++i) tht_l += fabs(xft[i] - xtn[i]);
@@ -1738,11 +1776,13 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #pragma unroll
               for (int i = 0; i < NX; ++i) r[i] = gq[i] - le[i];
               if (hasU) {
+                if (k > 0)  // (X_0 enters only g_0)
 #pragma unroll
-                for (int j = 0; j < NX; ++j)
+                  for (int j = 0; j < NX; ++j)
 #pragma unroll
-                  for (int m = 0; m < NX; ++m)
-                    if (Model::AMASK & (1ull << (m * NX + j))) r[j] = fma(Model::jacA(ctx, A)[m * NX + j], lnx[m], r[j]);
+                    for (int m = 0; m < NX; ++m)
+                      if (Model::AMASK & (1ull << (m * NX + j)))
+                        r[j] = fma(Model::jacA(ctx, A)[m * NX + j], lnx[m], r[j]);
 #pragma unroll
                 for (int l = 0; l < NU; ++l) {
                   double acc = gq[NX + l];
@@ -1812,8 +1852,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
                            __attribute__((always_inline)) {
       double xtn[NX];
       group_next<G, NX>(zt, xtn, xw);
-      double xft[NX], qt;
-      Model::value(ma, ctx, zt, xft, qt);
+      double xft[NX], qt, ze[NZ];
+      stage_point(zt, ze);
+      Model::value(ma, ctx, ze, xft, qt);
       double tht_l = 0, pht_l = 0;
 #pragma unroll
       for (int i = 0; i < NX; ++i) {
@@ -1987,6 +2028,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
                 xw.sync();
               }
             }
+            if (k == 0)  // p_0 of the correction: the barrier gradient (A_0 = 0, K_0 = 0)
+#pragma unroll
+              for (int i = 0; i < NX; ++i) pv[i] = gp[i];
             double dzs[NZ], dls[NX];
             forward(cs, kfs, pv, cs0, dzs, dls);
             // primal and dual fraction to the boundary along the correction
@@ -2340,7 +2384,8 @@ __global__ void shift_kernel(SolveArgs a, double* __restrict__ P, const double* 
   }
 }
 
-// Constraint values g = [x0 - X_0; F(X_k, U_k) - X_{k+1}] (Casadi/multiple_shooting_casadi.py:131,172-175).
+// Constraint values g = [x0 - X_0; F(X~_k, U_k) - X_{k+1}] with X~_0 = x0 and X~_k = X_k for k >= 1
+// (Casadi/multiple_shooting_casadi.py:125,131,157,172-175: interval 0 integrates from the parameter).
 template <class Model>
 __global__ void constraints_kernel(SolveArgs a, const double* __restrict__ W, double* __restrict__ Gout) {
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU;
@@ -2356,7 +2401,7 @@ __global__ void constraints_kernel(SolveArgs a, const double* __restrict__ W, do
     typename Model::Ctx ctx;
     Model::load_ctx(ma, b, p, kk, true, ctx);
     double z[NZ], xf[NX], q;
-    for (int i = 0; i < NX; ++i) z[i] = w[ixw<NX, NU>(kk, i)];
+    for (int i = 0; i < NX; ++i) z[i] = kk == 0 ? p[i] : w[ixw<NX, NU>(kk, i)];
     for (int i = 0; i < NU; ++i) z[NX + i] = w[iuw<NX, NU>(kk, i)];
     Model::value(ma, ctx, z, xf, q);
     for (int i = 0; i < NX; ++i) g[NX * (kk + 1) + i] = xf[i] - w[ixw<NX, NU>(kk + 1, i)];

@@ -227,8 +227,16 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const
   io.status = -1;
   io.it_next = io.it + 1;
 
-  // ---- evaluation at (zz, ll): derivatives (objective scaled by fse) and the defects
+  // ---- evaluation at (zz, ll): derivatives (objective scaled by fse) and the defects.  As in the
+  //      solve loop, interval 0 integrates from the parameter x0 (X_0 enters only g_0): lane 0
+  //      evaluates at (x0, U_0), has no x-gradient, and its Newton step treats A_0 as zero
   double xf[NX], qv, A[NX * NX], Bm[NX * NU], gq[NZ], Hs[NH], cdef[NX], c0[NX], ln[NX];
+  auto stage_point = [&](const double* zz, double* ze) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i) ze[i] = (k == 0) ? x0[i] : zz[i];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) ze[NX + i] = zz[NX + i];
+  };
   auto evaluate = [&](const double* zz, const double* ll, double fse) __attribute__((always_inline)) {
     double own_[2 * NX], nxt[2 * NX], xn[NX];
 #pragma unroll
@@ -242,13 +250,15 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const
       ln[i] = nxt[i];
       xn[i] = nxt[NX + i];
     }
-    Model::derivs(ma, ctx, zz, ln, fse, xf, qv, A, Bm, gq, Hs);
-    const double m = hasU ? 1.0 : 0.0;
+    double ze[NZ];
+    stage_point(zz, ze);
+    Model::derivs(ma, ctx, ze, ln, fse, xf, qv, A, Bm, gq, Hs);
+    const double m = hasU ? 1.0 : 0.0, mx = (hasU && k > 0) ? 1.0 : 0.0;
     qv *= m;
 #pragma unroll
     for (int i = 0; i < NH; ++i) Hs[i] *= m;
 #pragma unroll
-    for (int i = 0; i < NZ; ++i) gq[i] *= m;
+    for (int i = 0; i < NZ; ++i) gq[i] *= (i < NX) ? mx : m;
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
       cdef[i] = hasU ? xf[i] - xn[i] : 0.0;
@@ -257,9 +267,10 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const
   };
   // value at zz: the defects (set 1 on lanes with an interval, set 0 on lane 0) and the stage cost
   auto value_c = [&](const double* zz, double* c1, double* cz, double& q) __attribute__((always_inline)) {
-    double xn[NX], xft[NX];
+    double xn[NX], xft[NX], ze[NZ];
     group_next<G, NX>(zz, xn, xw);
-    Model::value(ma, ctx, zz, xft, q);
+    stage_point(zz, ze);
+    Model::value(ma, ctx, ze, xft, q);
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
       c1[i] = hasU ? xft[i] - xn[i] : 0.0;
@@ -275,11 +286,12 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const
 #pragma unroll
       for (int i = 0; i < NX; ++i) r[i] = gq[i] - ll[i];
       if (hasU) {
+        if (k > 0)  // (X_0 enters only g_0)
 #pragma unroll
-        for (int j = 0; j < NX; ++j)
+          for (int j = 0; j < NX; ++j)
 #pragma unroll
-          for (int m = 0; m < NX; ++m)
-            if (Model::AMASK & (1ull << (m * NX + j))) r[j] = fma(A[m * NX + j], ln[m], r[j]);
+            for (int m = 0; m < NX; ++m)
+              if (Model::AMASK & (1ull << (m * NX + j))) r[j] = fma(A[m * NX + j], ln[m], r[j]);
 #pragma unroll
         for (int l = 0; l < NU; ++l) {
           double acc = gq[NX + l];
@@ -687,6 +699,14 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const
           xw.sync();
         }
       }
+      if (k == 0) {  // node 0 (A_0 = 0, no x blocks in stage 0): P_0 = Sigma_x + delta, p_0 = gp_x
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+#pragma unroll
+          for (int j = i; j < NX; ++j) P[symix(i, j, NX)] = (i == j) ? sig[i] + delta : 0.0;
+          p[i] = gp[i];
+        }
+      }
 #pragma unroll
       for (int i = 0; i < NP; ++i) Pk[i] = P[i];
 #pragma unroll
@@ -717,6 +737,9 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const
     }
     double Kk[NU * NX], kfk[NU];
     riccati_gains<NX, NU>(fac, Kk, kfk);
+    if (k == 0)  // Hux'_0 = 0 (A_0 = 0)
+#pragma unroll
+      for (int i = 0; i < NU * NX; ++i) Kk[i] = 0.0;
     // ---- forward pass, node by node: node j+1 lands through its row block,
     //      dx_{j+1} = S^-1 (D^-1 y - p_{j+1}), y = A dx_j + B du_j + ct, S = D^-1 + P_{j+1}
     double Pv[NP + NX], Pn1[NP + NX];
@@ -747,8 +770,9 @@ __device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const
 #pragma unroll
       for (int r = 0; r < NX; ++r) {
         double acc = ct1[r];
+        if (k > 0)  // dx_1 does not depend on dx_0 (A_0 = 0)
 #pragma unroll
-        for (int m = 0; m < NX; ++m) acc = fma(A[r * NX + m], dxk[m], acc);
+          for (int m = 0; m < NX; ++m) acc = fma(A[r * NX + m], dxk[m], acc);
 #pragma unroll
         for (int l = 0; l < NU; ++l) acc = fma(Bm[r * NU + l], du[l], acc);
         y[r] = acc;

@@ -118,11 +118,15 @@ MPCX_DECLARE(cartpole)
 // horizons from which the unicycle's Riccati recursion runs as a log-depth scan (models.h
 // UnicycleScanModel): ceil(log2(N+1)) = 5 combine levels cost about as much as 25 chain steps
 constexpr int kUnicycleScanMinN = 25;
-// diagnostic knob: MPCX_UNICYCLE_SCAN_MIN_N overrides it (A/B of the two instantiations)
+// diagnostic knob: MPCX_UNICYCLE_SCAN_MIN_N overrides it (A/B of the two instantiations).  Only
+// a whole number in [1, 256] is taken (256: the scan never runs); anything else keeps the default.
 static int unicycle_scan_min_n() {
   static const int n = [] {
     const char* e = getenv("MPCX_UNICYCLE_SCAN_MIN_N");
-    return e ? atoi(e) : kUnicycleScanMinN;
+    if (!e || !*e) return kUnicycleScanMinN;
+    char* end = nullptr;
+    const long v = strtol(e, &end, 10);
+    return (*end == '\0' && v >= 1 && v <= 256) ? (int)v : kUnicycleScanMinN;
   }();
   return n;
 }

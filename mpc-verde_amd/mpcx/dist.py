@@ -30,6 +30,30 @@ def device_index(local_rank: int) -> int:
     return int(forced) if forced is not None else local_rank
 
 
+def visible_gpu_count(topology="/sys/class/kfd/kfd/topology/nodes", environ=None):
+    """GPUs this process may use, counted WITHOUT touching HIP (a launcher decides how many ranks
+    to start before any GPU call): the KFD topology's GPU nodes (gpu_id != 0), capped by
+    ROCR_/HIP_/CUDA_VISIBLE_DEVICES when set.  None when the topology cannot be read (each rank
+    then checks its own device)."""
+    environ = os.environ if environ is None else environ
+    try:
+        nodes = os.listdir(topology)
+    except OSError:
+        return None
+    n = 0
+    for d in nodes:
+        try:
+            with open(os.path.join(topology, d, "gpu_id")) as f:
+                n += int(f.read().strip() or "0") != 0
+        except (OSError, ValueError):
+            pass
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def backend(default: str = "nccl") -> str:
     """Process-group backend: RCCL ("nccl") unless MPCX_DIST_BACKEND overrides it (gloo for
     the one-GPU rehearsal above: RCCL needs a distinct GPU per rank)."""

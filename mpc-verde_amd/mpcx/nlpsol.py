@@ -189,8 +189,12 @@ class Solver:
 
     def lam_x_from_kkt(self, w, P, lam_g):
         """Bound multipliers reconstructed from stationarity, grad f + J^T lam_g + lam_x = 0
-        (evaluated with the sweep kernel; used to cross-check the solver's own lam_x)."""
-        s = self.rk4_sens(w, P)
+        (evaluated with the sweep kernel; used to cross-check the solver's own lam_x).  Interval 0
+        integrates from x0 = P[:3] (multiple_shooting_casadi.py:125,157), so X_0 enters only g_0."""
+        we = np.array(np.atleast_2d(w), np.float64)
+        P2 = np.atleast_2d(np.asarray(P, np.float64))
+        we[:, 0:3] = P2[:, 0:3]  # the sweep evaluates interval 0 at (x0, U_0)
+        s = self.rk4_sens(we, P2)
         B, N = s["q"].shape
         r = np.zeros((B, self._h.n_w))
         lam_g = np.asarray(lam_g).reshape(B, -1)
@@ -198,7 +202,8 @@ class Solver:
         r[:, 0:3] -= lam_g[:, 0:3]
         for k in range(N):
             l1 = lam_g[:, 3 * (k + 1):3 * (k + 2)]
-            r[:, ix(k)] += s["gq"][:, k, 0:3] + np.einsum("bij,bi->bj", s["A"][:, k], l1)
+            if k > 0:
+                r[:, ix(k)] += s["gq"][:, k, 0:3] + np.einsum("bij,bi->bj", s["A"][:, k], l1)
             r[:, 3 + 5 * k:5 + 5 * k] += s["gq"][:, k, 3:5] + np.einsum("bij,bi->bj", s["B"][:, k], l1)
             r[:, ix(k + 1)] -= l1
         return -r

@@ -87,8 +87,8 @@ class ControlSolver:
         self.ocp = ocp
         self._lin_blocked = isinstance(ocp, LinearOCP) and ocp.nx == 5 and ocp.nu == 1 and hasattr(ocp, "A_plant")
         if ocp.param != "x0_stageref" and not self._lin_blocked:
-            raise ValueError("nmpc: problems with per-stage parameters (param 'x0_stageref') or the move-blocked "
-                             "QP of lti.inverted_pendulum_qp")
+            raise ValueError("nmpc supports only problems with param 'x0_stageref' (per-stage parameters) or the "
+                             f"move-blocked QP of lti.inverted_pendulum_qp (got param={ocp.param!r})")
         self._solver = nlpsol("nmpc", "mi355x", ocp, opts or {}, device=device)
         N = ocp.N
         self._nxu = (4, 1) if self._lin_blocked else (ocp.nx, ocp.nu)

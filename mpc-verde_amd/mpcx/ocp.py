@@ -145,6 +145,10 @@ def to_spec(ocp, max_iter=2000, tol=1e-8, device=0, warm=(1e-4, 1e-4, 1e-4), gro
     for k in IPOPT_OPTIONS:
         if k == "acceptable_iter":
             s.acceptable_iter = -1 if int(o[k]) == 0 else int(o[k])  # IPOPT: 0 disables the heuristic
+        elif k == "acceptable_obj_change_tol" and float(o[k]) == 0.0:
+            # the spec reads a 0 field as IPOPT's default (include/mpcx.h); IPOPT's literal 0
+            # (|f - f_last| <= 0) is the same test as |f - f_last| <= 5e-324 max(1, |f|)
+            s.acceptable_obj_change_tol = 5e-324
         else:
             setattr(s, k, float(o[k]))
     s.no_restoration = 0 if restoration else 1

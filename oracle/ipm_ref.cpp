@@ -402,9 +402,12 @@ void evaluate(const Inst<Dyn>& I, const double* w, const double* lam, bool deriv
   }
   for (int i = 0; i < NX; ++i) e.c[i] = I.x0[i] - w[I.ix(0, i)];
   for (int k = 0; k < N; ++k) {
+    // interval 0 integrates from the parameter x0 (Casadi/multiple_shooting_casadi.py:125,157:
+    // Xk = P[:n_states], F(x0=vertcat(Xk, P[3:]), p=U_0)): the lifted X_0 enters only g_0, so
+    // stage 0 has no derivative with respect to it (A_0 = 0, no x-gradient, no x Hessian blocks)
     double xk[NX], uk[NU], xn[NX];
     for (int i = 0; i < NX; ++i) {
-      xk[i] = w[I.ix(k, i)];
+      xk[i] = k == 0 ? I.x0[i] : w[I.ix(k, i)];
       xn[i] = w[I.ix(k + 1, i)];
     }
     for (int i = 0; i < NU; ++i) uk[i] = w[I.iu(k, i)];
@@ -419,6 +422,15 @@ void evaluate(const Inst<Dyn>& I, const double* w, const double* lam, bool deriv
     }
     Jet<NZ> xf[NX], qf;
     stage_jet<Dyn>(*I.pb, zr, xk, uk, xf, qf);
+    if (k == 0) {  // x0 is a parameter of interval 0: drop the x directions of its jets
+      auto drop_x = [&](Jet<NZ>& j) {
+        for (int a = 0; a < NX; ++a) j.g[a] = 0.0;
+        for (int a = 0; a < NX; ++a)
+          for (int b = a; b < NZ; ++b) j.h[hix<NZ>(a, b)] = 0.0;
+      };
+      for (int r = 0; r < NX; ++r) drop_x(xf[r]);
+      drop_x(qf);
+    }
     e.f += I.fscale * qf.v;
     e.qsum += qf.v;
     for (int i = 0; i < NX; ++i) e.c[NX * (k + 1) + i] = xf[i].v - xn[i];

@@ -192,11 +192,15 @@ def stage_refs(P, ocp: UnicycleOCP, pstage=None):
 
 
 def ms_functions(w, P, ocp: UnicycleOCP, pstage=None):
-    """Objective and constraints of the multiple-shooting NLP (``:141-178``)."""
+    """Objective and constraints of the multiple-shooting NLP (``:141-178``).  Interval 0
+    integrates from the parameter (``Xk = P[:n_states]`` at ``:125``, ``F(x0=vertcat(Xk,
+    P[3:]), p=Uk)`` at ``:157``): the lifted X_0 enters only g_0."""
     N = ocp.N
     X, U = split_w(w, N)
     xr, ur = stage_refs(P, ocp, pstage)
-    xf, qf = F(X[..., :-1, :], U, xr, ocp, ur)
+    Xs = X[..., :-1, :].copy()
+    Xs[..., 0, :] = np.asarray(P)[..., 0:3]
+    xf, qf = F(Xs, U, xr, ocp, ur)
     J = qf.sum(axis=-1)
     g0 = np.asarray(P)[..., 0:3] - X[..., 0, :]
     gk = xf - X[..., 1:, :]

@@ -207,10 +207,13 @@ class Problem:
         return X, U
 
     def kkt_residual(self, w, lam_g, lam_x, P):
-        """max |grad f + J_g^T lam_g + lam_x| and max |g| at a multiple-shooting point."""
+        """max |grad f + J_g^T lam_g + lam_x| and max |g| at a multiple-shooting point.  Interval 0
+        integrates from the parameter x0 (multiple_shooting_casadi.py:125,157): X_0 enters only g_0."""
         nx, nu, nz, N = self.nx, self.nu, self.nz, self.N
         X, U = self.split_w(np.asarray(w, float))
-        Z = np.concatenate([X[:-1], U], axis=1)
+        Xs = X[:-1].copy()
+        Xs[0] = np.asarray(P[:nx], float)
+        Z = np.concatenate([Xs, U], axis=1)
         zr = self.refs(P)
         Jac = self.jac(Z)
         gl = 2 * self.W * (Z - zr)
@@ -220,9 +223,10 @@ class Problem:
         r[ix(0)] -= lam_g[0]
         for k in range(N):
             l1 = lam_g[k + 1]
-            r[ix(k)] += gl[k, :nx] + Jac[k, :, :nx].T @ l1
+            if k > 0:
+                r[ix(k)] += gl[k, :nx] + Jac[k, :, :nx].T @ l1
             r[nx + nz * k: nx + nz * k + nu] += gl[k, nx:] + Jac[k, :, nx:].T @ l1
             r[ix(k + 1)] -= l1
         r += np.asarray(lam_x, float)
-        gres = np.concatenate([np.asarray(P[:nx], float) - X[0]] + [self.F(X[k], U[k]) - X[k + 1] for k in range(N)])
+        gres = np.concatenate([np.asarray(P[:nx], float) - X[0]] + [self.F(Xs[k], U[k]) - X[k + 1] for k in range(N)])
         return float(np.max(np.abs(r))), float(np.max(np.abs(gres)))

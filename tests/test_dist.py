@@ -141,3 +141,18 @@ def test_bench_gpus_mismatch_exits_nonzero():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr and r.stdout == ""
+
+
+def test_visible_gpu_count_reads_topology_without_hip(tmp_path):
+    """bench.py decides its launch plan on mdist.visible_gpu_count(): the KFD topology's GPU
+    nodes (gpu_id != 0; CPU nodes have gpu_id 0), capped by *_VISIBLE_DEVICES, no HIP call."""
+    from mpcx import dist as mdist
+
+    for i, gid in enumerate([0, 0, 1234, 5678, 91011]):  # two CPU nodes, three GPUs
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "gpu_id").write_text(f"{gid}\n")
+    assert mdist.visible_gpu_count(str(tmp_path), environ={}) == 3
+    assert mdist.visible_gpu_count(str(tmp_path), environ={"HIP_VISIBLE_DEVICES": "0,2"}) == 2
+    assert mdist.visible_gpu_count(str(tmp_path), environ={"ROCR_VISIBLE_DEVICES": "1"}) == 1
+    assert mdist.visible_gpu_count(str(tmp_path / "missing"), environ={}) is None

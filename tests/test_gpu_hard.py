@@ -198,3 +198,29 @@ def test_park_and_resume_through_device_loop(mpcx):
     for n in ("w", "w0", "lam", "lamx", "f"):
         np.testing.assert_array_equal(getattr(run, n).cpu().numpy(), getattr(fused, n).cpu().numpy(), err_msg=n)
     np.testing.assert_array_equal(run.P.cpu().numpy()[:, 0:6], fused.P.cpu().numpy()[:, 0:6])
+
+
+def test_park_slots_cleared_between_batch_sizes(mpcx):
+    """A handle's restoration workspace is laid out by each launch's thread count.  A parking
+    launch at B = 1024 followed by a parking launch at B = 8 on the SAME handle must give, bit for
+    bit, what a fresh handle gives for the 8 instances (and what the big launch gave for them):
+    the solve launch clears every thread's park slot, so the resume launch sees only the instances
+    its own solve launch parked (config-4 6-state bicycle; 262, 483 and 10 park from the cold
+    start)."""
+    from mpcx import dist as mdist
+
+    N = 50
+    ocp = mpcx.dynamic_bicycle_lane_change(N=N)
+    t0, x0, (X, Y, V) = mdist.config4_bicycle_inputs(0, 1024)
+    refs = np.stack([mpcx.ode.dyn_bicycle_references(X, Y, V, int(t), N).reshape(-1) for t in t0])
+    P = ocp.params(x0, refs)
+    opts = {"ipopt": {"max_iter": 3000}}
+    reused = mpcx.nlpsol("reused", "mi355x", ocp, opts)
+    big = reused.solve_batch(P)
+    assert np.all(big["status"] <= 1), np.flatnonzero(big["status"] > 1)
+    idx = [0, 262, 1, 2, 3, 4, 5, 6]
+    small = reused.solve_batch(P[idx])
+    fresh = mpcx.nlpsol("fresh", "mi355x", ocp, opts).solve_batch(P[idx])
+    for n in ("w", "f", "lam_g", "lam_x", "status", "iters"):
+        np.testing.assert_array_equal(small[n], fresh[n], err_msg=n)
+        np.testing.assert_array_equal(small[n], big[n][idx], err_msg=n)

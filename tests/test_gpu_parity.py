@@ -233,6 +233,40 @@ def test_kkt_residual_at_solution(mpcx, R):
         assert pg < 1e-5
 
 
+def test_interval0_integrates_from_parameter(mpcx, R, C):
+    """Interval 0 as the script formulates it: Xk = P[:3] (:125) and F(x0=vertcat(Xk, P[3:]),
+    p=U_0) (:157), so the lifted X_0 enters only g_0 = P[:3] - X_0 (:128-136) and CasADi's
+    lam_g[0:3] is 0.  Cold start (X_0 = P[:3]): lam_g[0:3] exactly 0.  From guesses whose X_0 is
+    NOT P[:3] (X_0 moved by up to 0.5, the shifted guess of the previous step's solution): the
+    same optimum, lam_g[0:3] = 0 to the dual tolerance, g = F(P[:3], U_0) - X_1 at the solution,
+    and the C++ oracle (same formulation) takes the same iteration counts from the same guess."""
+    N, B = 20, 256
+    ocp = mpcx.unicycle_point_to_point(N=N)
+    solver = mpcx.nlpsol("s", "mi355x", ocp, {"ipopt": {"max_iter": 2000, "acceptable_tol": 1e-8,
+                                                        "acceptable_obj_change_tol": 1e-6}})
+    P = config2_batch(B, seed=11)
+    cold = solver.solve_batch(P, want_g=True)
+    assert np.all(cold["status"] == 0)
+    assert np.all(cold["lam_g"][:, 0:3] == 0.0), np.abs(cold["lam_g"][:, 0:3]).max()
+    w0 = cold["w"].copy()
+    w0[:, 0:3] += np.random.default_rng(4).uniform(-0.5, 0.5, (B, 3))
+    r = solver.solve_batch(P, w0=w0, want_g=True)
+    assert np.all(r["status"] <= 1)
+    assert np.max(np.abs(r["lam_g"][:, 0:3])) <= 1e-8
+    assert np.max(np.abs(r["g"])) <= 1e-9
+    errs = np.array([rel_err(r["w"][b], cold["w"][b]) for b in range(B)])
+    assert errs.max() <= 1e-5, errs.max()  # the same optimum to the solve tolerance (measured 1.2e-6)
+    # the constraint values returned are g_1 = F(P[:3], U_0) - X_1 (not F(X_0, U_0) - X_1)
+    xf, _ = R.F(P[:, 0:3], r["w"][:, 3:5], P[:, 3:6], R.UnicycleOCP(N=N))
+    np.testing.assert_allclose(r["g"][:, 3:6], xf - r["w"][:, 5:8], atol=1e-12)
+    ref = C.solve(R.UnicycleOCP(N=N), P, w0=w0, nthreads=0, max_iter=2000, acceptable_tol=1e-8,
+                  acceptable_obj_change_tol=1e-6)
+    n_it = int(np.sum(ref["iters"] != r["iters"]))
+    print(f"interval 0 from x0: {n_it} of {B} iteration counts differ from the C++ oracle (X_0 != x0 guesses)")
+    assert n_it == 0, np.flatnonzero(ref["iters"] != r["iters"])
+    assert np.max(np.abs(ref["lam_g"][:, 0:3])) <= 1e-8
+
+
 # ----------------------------------------------------------------------------- edge cases
 @pytest.mark.parametrize("B", [1, 2, 3, 31, 33, 65])
 def test_ragged_batch_sizes(mpcx, R, B):

@@ -106,13 +106,15 @@ def test_oracle_single_shooting_optimum_is_ms_kkt_point(which):
     U, X, info = pr.solve(P)
     assert info["status"] == "converged"
     _, g, _, _ = pr.derivatives(U, P)
-    # lam_g = adjoint states, lam_x(u) = -reduced gradient (nonzero only on active bounds)
+    # lam_g = adjoint states, lam_x(u) = -reduced gradient (nonzero only on active bounds); the
+    # multiplier of g_0 is 0: interval 0 integrates from the parameter x0, so X_0 enters only g_0
+    # (Casadi/multiple_shooting_casadi.py:125,157)
     nx, nu, nz, N = pr.nx, pr.nu, pr.nz, pr.N
     Z = np.concatenate([X[:-1], U], axis=1)
     Jac = pr.jac(Z)
     gl = 2 * pr.W * (Z - pr.refs(P))
     lam = np.zeros((N + 1, nx))
-    for k in range(N - 1, -1, -1):
+    for k in range(N - 1, 0, -1):
         lam[k] = gl[k, :nx] + Jac[k, :, :nx].T @ lam[k + 1]
     lam_x = np.zeros(nx + nz * N)
     for k in range(N):
