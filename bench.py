@@ -118,6 +118,8 @@ def parse():
     ap.add_argument("--roofline-reps", type=int, default=20)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dump-stats", default=None,
+                    help="rank 0 saves the all-gathered per-instance statistics (global instance order) to this .npy")
     ap.add_argument("--no-reference-warm-start", action="store_true",
                     help="skip the second timing under the reference's warm start (shifted primal only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum timed CPU-baseline solve time")
@@ -640,6 +642,8 @@ def main():
     S = mdist.stats_matrix(P_fin_of(loop), None, loop.f.cpu().numpy(), status_hist.max(dim=0).values.cpu().numpy(),
                            iters_hist.cpu().numpy())
     S_all = mdist.all_gather_stats(S, device=loop.P.device)
+    if rank == 0 and args.dump_stats:
+        np.save(args.dump_stats, S_all)  # (global batch, STAT_FIELDS): shard-exactness tests
     iters_max_step = res["iters_max_step"]
 
     # group-iterations of every solve launch of this run, both policies (PMC normalisation,

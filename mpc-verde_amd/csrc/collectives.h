@@ -135,6 +135,30 @@ template <int G>
 __device__ __forceinline__ double gmin(double v, XWave<G>& xw) {
   return greduce<G, OpMin>(v, xw);
 }
+// Group tests by ballot: true on every lane of the group iff c holds on all of its (active) lanes.
+// A threshold test on a group max -- max_k e_k <= t -- is the group test of e_k <= t (max is exact),
+// so the solve loop's convergence, acceptable-level and barrier tests need no max reduction (a
+// 5-6 level DPP/permlane chain of ~25 instructions) but one ballot.  L = lanes of one instance in
+// the wave: G, or 64 for a replicated 32-lane group (kernels.h R = 2), whose test is wave-uniform.
+template <int G, int L = G>
+__device__ __forceinline__ bool gall(bool c, XWave<G>& xw) {
+  if constexpr (G > 64) {
+    return greduce<G, OpMin>(c ? 1.0 : 0.0, xw) > 0.5;
+  } else {
+    const unsigned long long f = __ballot(!c);  // lanes where c fails
+    if constexpr (L >= 64) {
+      return f == 0;
+    } else {
+      const int sh = (int)(threadIdx.x & 63) & ~(G - 1);
+      return ((f >> sh) & ((1ull << G) - 1)) == 0;
+    }
+  }
+}
+template <int G, int L = G>
+__device__ __forceinline__ bool gany(bool c, XWave<G>& xw) {
+  return !gall<G, L>(!c, xw);
+}
+
 // value of lane k+1 / k-1 (whole-wave DPP shift; groups are contiguous and the lanes
 // that would read across a group boundary never use the value)
 __device__ __forceinline__ double from_next(double v) { return dpp<kWaveShl1>(v); }

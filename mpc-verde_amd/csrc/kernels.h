@@ -164,7 +164,7 @@ struct FilterLds {
     return r;
   }
   __device__ __forceinline__ bool contains(double t, double q, XWave<G>& xw) const {
-    return n > 0 && gmax<G>(covers(t, q) ? 1.0 : 0.0, xw) > 0.5;
+    return n > 0 && gany<G>(covers(t, q), xw);
   }
   __device__ __forceinline__ bool add(double nth, double nph, int k, XWave<G>& xw) {
     if (n < kCap) {  // append
@@ -225,25 +225,24 @@ struct LdsCol {
   __device__ __forceinline__ void relaunder() { asm volatile("" : "+v"(off)); }
 };
 
-#ifndef MPCX_DEC_TIGHT
-#define MPCX_DEC_TIGHT 1
-#endif
-#ifndef MPCX_CHAIN_EARLY_EXIT
-#define MPCX_CHAIN_EARLY_EXIT true
-#endif
-#ifndef MPCX_DEC_SCAN
-#define MPCX_DEC_SCAN true
-#endif
-#ifndef MPCX_SOFT_INLINE
-#define MPCX_SOFT_INLINE true
-#endif
-#ifndef MPCX_WAVES_PER_EU
-#define MPCX_WAVES_ATTR
-#else
-#define MPCX_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(MPCX_WAVES_PER_EU, MPCX_WAVES_PER_EU)))
-#endif
-template <class Model, int G, bool RESUME = false>
-__global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(SolveArgs a) {
+// Model::kReplicate if the model declares it: a 32-lane group may run replicated (R = 2, below)
+template <class M, class = void>
+struct ReplicateOf {
+  static constexpr bool value = false;
+};
+template <class M>
+struct ReplicateOf<M, std::void_t<decltype(M::kReplicate)>> {
+  static constexpr bool value = M::kReplicate;
+};
+
+// R = 2 (replicated groups, G = 32): a batch too small to give every SIMD a wave runs one
+// instance per wave with its lane group held TWICE, in the wave's two 32-lane halves (replica rho
+// = lane / 32).  Both replicas compute the same bits (every collective is a 32-lane group
+// collective, as for two instances per wave); only replica 0 writes results.  The sequential
+// phases split their work between the replicas.
+template <class Model, int G, bool RESUME = false, int R = 1>
+__global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArgs a) {
+  static_assert(R == 1 || (R == 2 && G == 32), "replicated groups: two 32-lane replicas per wave");
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2, NP = NX * (NX + 1) / 2;
   // resume launch: nothing parked by this step's solve launch -> return before any setup
   if constexpr (RESUME)
@@ -280,7 +279,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     return (const double*)__builtin_assume_aligned(r, 16);
   };
   XWave<G> xw{xch, 0};
-  const int inst = (int)(gid / G);
+  const int inst = (int)(gid / (G * R));
+  const int rho = R > 1 ? (int)((threadIdx.x / G) % R) : 0;  // replica of this lane (0: the writer)
   const bool valid = inst < a.B;
   const int N = a.N;
   const int nw = NX + NZ * N, ng = NX * (N + 1);
@@ -464,7 +464,10 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     }
     double ze[NZ];
     stage_point(zz, ze);
-    Model::derivs(ma, ctx, ze, ln, fs, xf, qv, A, Bm, gq, Hs);
+    if constexpr (R > 1)  // the replicas split the evaluation's sequential RK4 substeps
+      Model::derivs_rep(ma, ctx, ze, ln, fs, xf, qv, A, Bm, gq, Hs, rho);
+    else
+      Model::derivs(ma, ctx, ze, ln, fs, xf, qv, A, Bm, gq, Hs);
     const double m = hasU ? 1.0 : 0.0, mx = (hasU && k > 0) ? 1.0 : 0.0;  // no x-gradient at X_0
     qv *= m;
     if constexpr (!Model::kTableHess)
@@ -514,7 +517,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   // soft restoration step in the solve loop (a cold block after the line search).  Only the
   // restoration phase proper parks the instance for the resume launch, so an instance whose line
   // search fails once does not serialise the rest of a multi-step launch.
-  constexpr bool kSoftInline = MPCX_SOFT_INLINE && kRes && Model::kEvalInSearch && !Model::kSOC;
+  constexpr bool kSoftInline = kRes && Model::kEvalInSearch && !Model::kSOC;
   bool soft_tried = false;  // this iteration's soft trial failed (the resume launch skips it)
   bool soft = false;
   int soft_count = 0;
@@ -567,8 +570,8 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     group_next<G, NS>(own, nxt, xw);
     if (bnd) {
       if (k == 0 && valid) {  // lanes past the batch are done from the start: no status row of theirs
-        if (a.status) a.status[(size_t)step * a.B + inst] = status;
-        if (a.iters) a.iters[(size_t)step * a.B + inst] = its;
+        if (a.status && rho == 0) a.status[(size_t)step * a.B + inst] = status;
+        if (a.iters && rho == 0) a.iters[(size_t)step * a.B + inst] = its;
         double zp[NZ], xfp[NX], qp;
 #pragma unroll
         for (int i = 0; i < NX; ++i) zp[i] = x0[i];
@@ -875,18 +878,19 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
     }
 #pragma unroll
     for (int i = 0; i < NX; ++i) Ec = qmax_abs(qmax_abs(Ec, cdef[i]), c0[i]);
-    Ed = gmax<G>(Ed, xw);
-    Ec = gmax<G>(Ec, xw);
-    Ecomp0 = gmax<G>(Ecomp0, xw);
+    // Ed, Ec, Ecomp0 stay per lane: every test below is a threshold on their group maximum, which
+    // holds iff it holds on every lane (gall: one ballot instead of a max reduction each; max is
+    // exact and the division by a positive group-uniform scaling monotone, so the decisions are the
+    // ones the reduced values give)
     lam1 = gsum<G>(lam1, xw);
     z1 = gsum<G>(z1, xw);
     // IPOPT's scalings s_d = max(s_max, (|lam|_1 + |z|_1) / (m + n)) / s_max and s_c = max(s_max,
     // |z|_1 / n_b) / s_max are exactly 1 unless the sum exceeds s_max times the count (a rounded
-    // quotient that reaches s_max from above still gives 1): the IEEE divisions -- two group-
-    // uniform ~12-instruction sequences each -- only run on waves where some instance needs them
+    // quotient that reaches s_max from above still gives 1): the IEEE divisions -- group-uniform
+    // ~12-instruction sequences -- only run on waves where some instance needs them
     const bool sd1 = !(lam1 + z1 > kSmax * (double)(ng + nw));
     const bool sc1 = !(nbound > 0 && z1 > kSmax * nbound);
-    double sd = 1.0, sc = 1.0, Eds = Ed, Ecs = Ecomp0;  // Ed / s_d, Ecomp0 / s_c
+    double sd = 1.0, sc = 1.0, Eds = Ed, Ecs = Ecomp0;  // Ed / s_d, Ecomp0 / s_c (this lane's)
     if (__any(!sd1 || !sc1)) {
       if (!sd1) {
         sd = fmax(kSmax, (lam1 + z1) / (double)(ng + nw)) / kSmax;
@@ -897,16 +901,18 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         Ecs = Ecomp0 / sc;
       }
     }
-    const double E0 = fmax(fmax(Eds, Ec), Ecs);
+    const double E0 = fmax(fmax(Eds, Ec), Ecs);  // this lane's part of the scaled NLP error
     // IPOPT OptimalityErrorConvergenceCheck: tol with the unscaled dual infeasibility,
     // constraint violation and complementarity tests; then the acceptable level (all of
     // acceptable_* and the objective change from the previous iterate) for acceptable_iter
     // iterates in a row.  fcur = the scaled objective.
     const double fcur = fs * gsum<G>(hasU ? qv : 0.0, xw);
-    const bool acceptable_now = E0 <= a.acc_tol && Ed <= a.acc_dual_inf_tol * fs && Ec <= a.acc_constr_viol_tol &&
-                                Ecomp0 <= a.acc_compl_inf_tol * fs &&
-                                fabs(fcur - f_last) <= a.acc_obj_change_tol * fmax(1.0, fabs(fcur));
-    if (!done && E0 <= a.tol && Ed <= a.dual_inf_tol * fs && Ec <= a.constr_viol_tol && Ecomp0 <= a.compl_inf_tol * fs) {
+    const bool acceptable_now =
+        gall<G, G * R>(E0 <= a.acc_tol && Ed <= a.acc_dual_inf_tol * fs && Ec <= a.acc_constr_viol_tol &&
+                       Ecomp0 <= a.acc_compl_inf_tol * fs, xw) &&
+        fabs(fcur - f_last) <= a.acc_obj_change_tol * fmax(1.0, fabs(fcur));
+    if (gall<G, G * R>(E0 <= a.tol && Ed <= a.dual_inf_tol * fs && Ec <= a.constr_viol_tol &&
+                       Ecomp0 <= a.compl_inf_tol * fs, xw) && !done) {
       done = true;
       status = 0;
       its = it;
@@ -926,8 +932,11 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       its = a.max_iter;
     }
 #ifdef MPCX_DEBUG_PRINT
-    if (inst == 0 && (k % 64) == 0)
-      printf("OPT it=%d k=%d fs=%g Ed=%g Ec=%g E0=%g sd=%g lam1=%g z1=%g\n", it, k, fs, Ed, Ec, E0, sd, lam1, z1);
+    {
+      const double Edg = gmax<G>(Ed, xw), Ecg = gmax<G>(Ec, xw), E0g = gmax<G>(E0, xw);
+      if (inst == 0 && (k % 64) == 0)
+        printf("OPT it=%d k=%d fs=%g Ed=%g Ec=%g E0=%g sd=%g lam1=%g z1=%g\n", it, k, fs, Edg, Ecg, E0g, sd, lam1, z1);
+    }
 #endif
     if (__all((done && step == K - 1) || parked)) break;
     // multi-step launches: a wave whose instances all just finished a step skips the rest of
@@ -946,12 +955,11 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         Ecm = qmax_abs(Ecm, hL[i] ? (z[i] - lb[i]) * zL[i] - mu : 0.0);
         Ecm = qmax_abs(Ecm, hU[i] ? (ub[i] - z[i]) * zU[i] - mu : 0.0);
       }
-      Ecm = gmax<G>(Ecm, xw);
-      double Ecms = Ecm;  // Ecm / s_c
+      double Ecms = Ecm;  // Ecm / s_c (this lane's; the test is a group threshold test, as above)
       if (__any(!sc1))
         if (!sc1) Ecms = Ecm / sc;
       const double Emu = fmax(fmax(Eds, Ec), Ecms);
-      const bool dec = !done && (Emu <= kKappaEps * mu || (tiny_flag && rep == 0)) && mu > mu_min;
+      const bool dec = !done && (gall<G, G * R>(Emu <= kKappaEps * mu, xw) || (tiny_flag && rep == 0)) && mu > mu_min;
       if (dec && !done) DIAG(3);
       if (dec) {
         static_assert(kThetaMu == 1.5, "mu^theta_mu evaluated as mu * sqrt(mu)");
@@ -1161,7 +1169,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         // a loop of their own that moves only p (the same operations as the mixed loop's cheap
         // steps; A stays in the stage table: 25 more live registers here measured slower)
         int jc = N;
-        if constexpr (kDec && MPCX_DEC_TIGHT) {
+        if constexpr (kDec) {
           if (__all(reuse)) {
             XWave<64> xw1{nullptr, 0};
             jc = G >= 64 ? kb : (int)greduce<64, OpMax>((double)kb, xw1);  // max over the wave's groups
@@ -1175,7 +1183,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
         // NX-vector, the powers (A^T)^(2^l) formed once per factorisation by NX^2 threads in LDS.
         // log2(N) levels replace the suffix's N - jc dependent steps (config 5: 95 of 100).
         bool sscan = false;  // group-uniform
-        if constexpr (kDec && G > 64 && MPCX_DEC_SCAN) {
+        if constexpr (kDec && G > 64) {
           if (jc < N && !a.lin.per_instance && a.tabseq == nullptr) {
             const bool mine = k >= jc && k < N;
             const double ti = (double)((ctx.A - a.lin.A) / (NX * NX));  // my stage's table
@@ -1250,7 +1258,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
           }
           // models with a long chain step (the workspace-stash models, one instance per wave): a
           // failed inertia test ends the chain early (below)
-          constexpr bool kEarly = MPCX_CHAIN_EARLY_EXIT && kWsStash && !kDec && G == 64;
+          constexpr bool kEarly = kWsStash && !kDec && G == 64;
           bool early = false;
           // the chain: one step per node, lane j only.  Models without the decoupled suffix take
           // the inertia verdict of their step from its factors after the chain, on all lanes at
@@ -1383,7 +1391,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       for (int i = 0; i < NP; ++i) Pk[i] = P[i];
 #pragma unroll
       for (int i = 0; i < NX; ++i) pk[i] = p[i];
-      const bool ok = gmin<G>(okl ? 1.0 : 0.0, xw) > 0.5;
+      const bool ok = gall<G, G * R>(okl, xw);
       // IPOPT inertia correction (Algorithm IC)
       if (need) {
         if (ok) {
@@ -1618,9 +1626,9 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
       tiny_l = qmax(tiny_l, own ? fma(-10.0 * kEps, 1.0 + fabs(z[i]), fabs(dz[i])) : -1.0);
       if (own) gd_l += gp[i] * dz[i];
     }
-    const double amax = gmin<G>(amax_l, xw), tiny = gmax<G>(tiny_l, xw);
+    const double amax = gmin<G>(amax_l, xw);
     double az = gmin<G>(az_l, xw);  // dual step length (a second-order correction replaces it)
-    const bool tinystep = tiny < 0.0;
+    const bool tinystep = gall<G, G * R>(tiny_l < 0.0, xw);  // max over the group < 0
     if (!done && amax < 1.0) DIAG(4);
     if (!done && tinystep) DIAG(5);
     const double gd = gsum<G>(gd_l, xw);
@@ -2183,7 +2191,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
 #ifdef MPCX_STAMPS
       if (k == 0)
         printf("LSFAIL inst=%d step=%d it=%d mu=%.3e thk=%.6e phk=%.10e gd=%.3e amax=%.3e alpha=%.3e amin=%.3e "
-               "Ed=%.3e Ec=%.3e Ecomp=%.3e E0=%.3e fs=%.3e dw=%.1e\n",
+               "node-0 Ed=%.3e Ec=%.3e Ecomp=%.3e E0=%.3e fs=%.3e dw=%.1e\n",
                inst, step, it, mu, thk, phk, gd, amax, alpha, amin, Ed, Ec, Ecomp0, E0, fs, delta);
 #endif
       done = true;
@@ -2239,7 +2247,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   }
   STAMP(9);
 #ifdef MPCX_STAMPS
-  if (g_mpcx_diag && valid && active && k == 0)
+  if (g_mpcx_diag && valid && active && k == 0 && rho == 0)
     for (int i = 0; i < kDiag; ++i) g_mpcx_diag[(size_t)inst * kDiag + i] = diag[i];
   if (g_mpcx_stamps && !RESUME && (threadIdx.x & 63) == 0) {
     const long wv = gid / 64;
@@ -2257,7 +2265,7 @@ __global__ __launch_bounds__(G > 64 ? G : 64) MPCX_WAVES_ATTR void solve_kernel(
   if (inst == 0 && (k % 64) == 0)
     printf("END k=%d fs=%g mu=%g it=%d lam0=%g z0=%g zL=%g zU=%g\n", k, fs, mu, it, lam[0], z[0], zL[NX], zU[NX]);
 #endif
-  const bool writes = valid && !parked && active;  // parked: the resume launch writes them
+  const bool writes = valid && !parked && active && rho == 0;  // parked: the resume launch writes them
   if (writes) {
     double* w = a.w_out + (size_t)inst * nw;
     if (hasX)
@@ -2422,6 +2430,12 @@ static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
   const long threads = (long)a.B * G;
   const int bs = G > 64 ? G : 64;
   const int blocks = (int)((threads + bs - 1) / bs);
+  // a 32-lane group widened to a wave runs replicated (R = 2) where the model has that instantiation
+  if constexpr (ReplicateOf<Model>::value)
+    if (G == 64 && solve_group_size(a.N, a.B, a.n_simd, 1) == 32) {
+      hipLaunchKernelGGL((solve_kernel<Model, 32, false, 2>), dim3(blocks), dim3(64), 0, stream, a);
+      return hipGetLastError();
+    }
   if (G == 16) hipLaunchKernelGGL((solve_kernel<Model, 16>), dim3(blocks), dim3(64), 0, stream, a);
   else if (G == 32) hipLaunchKernelGGL((solve_kernel<Model, 32>), dim3(blocks), dim3(64), 0, stream, a);
   else if (G == 64) hipLaunchKernelGGL((solve_kernel<Model, 64>), dim3(blocks), dim3(64), 0, stream, a);
@@ -2440,6 +2454,11 @@ static hipError_t launch_resume_model(const SolveArgs& a, hipStream_t stream) {
     const long threads = (long)a.B * G;
     const int bs = G > 64 ? G : 64;
     const int blocks = (int)((threads + bs - 1) / bs);
+    if constexpr (ReplicateOf<Model>::value)
+      if (G == 64 && solve_group_size(a.N, a.B, a.n_simd, 1) == 32) {
+        hipLaunchKernelGGL((solve_kernel<Model, 32, true, 2>), dim3(blocks), dim3(64), 0, stream, a);
+        return hipGetLastError();
+      }
     if (G == 16) hipLaunchKernelGGL((solve_kernel<Model, 16, true>), dim3(blocks), dim3(64), 0, stream, a);
     else if (G == 32) hipLaunchKernelGGL((solve_kernel<Model, 32, true>), dim3(blocks), dim3(64), 0, stream, a);
     else if (G == 64) hipLaunchKernelGGL((solve_kernel<Model, 64, true>), dim3(blocks), dim3(64), 0, stream, a);

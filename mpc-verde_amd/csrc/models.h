@@ -11,27 +11,6 @@
 #include "solver.h"
 #include "unicycle.h"
 
-#ifndef MPCX_PSCAN_DEFAULT
-#define MPCX_PSCAN_DEFAULT true
-#endif
-#ifndef MPCX_SCAN_MAX_NX
-#define MPCX_SCAN_MAX_NX 4
-#endif
-#ifndef MPCX_PSCAN_UNICYCLE
-#define MPCX_PSCAN_UNICYCLE false
-#endif
-#ifndef MPCX_BOUNDS_LDS
-#define MPCX_BOUNDS_LDS false
-#endif
-#ifndef MPCX_BOUNDS_LDS_LIN
-#define MPCX_BOUNDS_LDS_LIN true
-#endif
-#ifndef MPCX_UNI_MOMENTS
-#define MPCX_UNI_MOMENTS true
-#endif
-#ifndef MPCX_UNICYCLE_RESTO
-#define MPCX_UNICYCLE_RESTO true
-#endif
 
 namespace mpcx {
 
@@ -53,12 +32,15 @@ struct UnicycleModel {
   // IPOPT's soft restoration and restoration phase (resto.h, the resume launch): a warm-started
   // closed-loop solve that sits at its optimum to rounding level can fail the filter line
   // search on noise in theta (tests/test_gpu_hard.py); IPOPT recovers it there
-  static constexpr bool kResto = MPCX_UNICYCLE_RESTO;
+  static constexpr bool kResto = true;
   // variable bounds in LDS, re-read per phase (kernels.h LdsCol): removes the kernel's scratch
   // spills but measured 1-2 % slower on config 2 (LDS latency on the line search), so off
-  static constexpr bool kBoundsLds = MPCX_BOUNDS_LDS;
+  static constexpr bool kBoundsLds = false;
   // backward Riccati recursion as a log-depth scan (pscan.h) instead of N dependent steps
-  static constexpr bool kParallelRiccati = MPCX_PSCAN_UNICYCLE;
+  static constexpr bool kParallelRiccati = false;
+  // a 32-lane group widened to a whole wave runs as two replicas that split the sequential work
+  // (kernels.h R = 2): configs 1-2 (N <= 30) at batches below two waves per SIMD
+  static constexpr bool kReplicate = true;
   struct Ctx {
     double xr[3], ur[2];
   };
@@ -81,10 +63,15 @@ struct UnicycleModel {
   __device__ __forceinline__ static void derivs(const ModelArgs& a, const Ctx& c, const double* z, const double* ln, double fs,
                                 double* xf, double& q, double* A, double* Bm, double* g, double* H) {
     const double u2[2] = {z[3], z[4]};
-    if constexpr (MPCX_UNI_MOMENTS)  // weighted-moment assembly (unicycle.h)
-      uni_derivs_moments(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H);
-    else
-      uni_derivs<true>(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H);
+    uni_derivs_moments(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H);  // weighted moments (unicycle.h)
+  }
+  // the same evaluation split between the two replicas of a replicated lane group (kernels.h R = 2;
+  // every lane of the wave must call it)
+  __device__ __forceinline__ static void derivs_rep(const ModelArgs& a, const Ctx& c, const double* z, const double* ln,
+                                                    double fs, double* xf, double& q, double* A, double* Bm, double* g,
+                                                    double* H, int rho) {
+    const double u2[2] = {z[3], z[4]};
+    uni_derivs_moments<2>(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H, rho);
   }
   __device__ __forceinline__ static void value(const ModelArgs& a, const Ctx& c, const double* z, double* xf, double& q) {
     const double u2[2] = {z[3], z[4]};
@@ -105,6 +92,7 @@ struct UnicycleFreeModel : UnicycleModel {
 // MI355X: config 3, N = 30, +6.5 % solves/s; config 2, N = 20, -4 %).
 struct UnicycleScanModel : UnicycleModel {
   static constexpr bool kParallelRiccati = true;
+  static constexpr bool kReplicate = false;  // no sequential chain to split
 };
 
 // ------------------------------------------------------------------------------------
@@ -133,7 +121,7 @@ struct LinearModel {
   // scan with register tables, 12.6 M scan with table operands; config 5 (NX = 5, N = 100)
   // 0.91 M sequential, 0.43 M / 0.87 M with the scan (its 65-double elements still spill), so
   // NX = 5 keeps the sequential recursion and register tables.
-  static constexpr bool kScan = MPCX_PSCAN_DEFAULT && NX_ <= MPCX_SCAN_MAX_NX;
+  static constexpr bool kScan = NX_ <= 4;
   static constexpr bool kParallelRiccati = kScan, kTableJac = kScan, kTableHess = kScan;
   // Decoupled suffix (solver.hip): the sequential recursion reuses P_k on a suffix of
   // decoupled stages -- the move-blocked stages of the cart-pole QP (lti.py).  Scan models
@@ -143,7 +131,7 @@ struct LinearModel {
   // registers held through every phase: A/B on one MI355X, config 5 (LinearModel<5,1>, G = 128)
   // scratch 704 -> 240 B/lane, 116 -> 100 us per IPM iteration (+15 % solves/s); config 4
   // (LinearModel<4,1>, scan) +3.5 %, scratch 404 -> 0 (LinearModel<4,2>: 680 -> 84)
-  static constexpr bool kBoundsLds = MPCX_BOUNDS_LDS_LIN;
+  static constexpr bool kBoundsLds = true;
   static constexpr int kTrigSlots = 0;
   __device__ __forceinline__ static const double* jacA(const Ctx& c, const double* A) { return kTableJac ? c.A : A; }
   __device__ __forceinline__ static const double* jacB(const Ctx& c, const double* B) { return kTableJac ? c.B : B; }

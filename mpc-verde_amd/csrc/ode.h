@@ -32,16 +32,6 @@
 #include "riccati.h"
 #include "solver.h"
 
-#ifndef MPCX_ODE_RESTO
-#define MPCX_ODE_RESTO true
-#endif
-#ifndef MPCX_BOUNDS_LDS_ODE
-#define MPCX_BOUNDS_LDS_ODE true
-#endif
-#ifndef MPCX_WS_STASH
-#define MPCX_WS_STASH true
-#endif
-
 namespace mpcx {
 
 using ::cos;  // the double overloads stay visible next to the HD ones below
@@ -278,17 +268,17 @@ struct OdeModel {
   static constexpr bool kSOC = Dyn::kSOC;
   // IPOPT's soft restoration and feasibility restoration phase (kernels.h; state in the
   // restoration workspace): the nonlinear models are the ones whose line searches fail
-  static constexpr bool kResto = MPCX_ODE_RESTO;
+  static constexpr bool kResto = true;
   // stage Hessian and Sigma of the 6-state model wait in the workspace across the inertia-
   // correction loop (kernels.h kWsStash): with them out of the registers the sequential chain's
   // operands no longer go through scratch once per step
-  static constexpr bool kWsStash = MPCX_WS_STASH && NX >= 6;
+  static constexpr bool kWsStash = NX >= 6;
   // variable bounds in LDS (kernels.h LdsCol) instead of 2 NZ doubles of registers held through
   // every phase.  A/B on one MI355X: cart-pole swing-up 122 -> 117 us per IPM iteration (scratch
   // 696 -> 204 B/lane), kinematic bicycle +1 % (scratch 400 -> 0); the 6-state bicycle, whose chain operands
   // already wait in the workspace, 3 % slower -- so not there
-  static constexpr bool kBoundsLds = MPCX_BOUNDS_LDS_ODE && NX < 6;
-  static constexpr bool kParallelRiccati = MPCX_PSCAN_DEFAULT && NX <= 5;  // NX = 6: LDS buffer too large
+  static constexpr bool kBoundsLds = NX < 6;
+  static constexpr bool kParallelRiccati = NX <= 5;  // NX = 6: LDS buffer too large
   struct Ctx {
     double zr[NZ];
   };

@@ -36,9 +36,6 @@
 #include "riccati.h"
 #include "solver.h"
 
-#ifndef MPCX_RECOVER_INLINE
-#define MPCX_RECOVER_INLINE __forceinline__  // called by the resume launch only
-#endif
 
 namespace mpcx {
 
@@ -158,9 +155,9 @@ struct RecIO {
 };
 
 template <class Model, int G>
-__device__ MPCX_RECOVER_INLINE void recover(RecIO& io, FilterLds<G>& filt, const ModelArgs ma,
-                                             const typename Model::Ctx ctx, double* wsl, const long wst,
-                                             const double* lbw, const double* ubw, double* xbuf) {
+// (inlined into the resume launch, its only caller)
+__device__ __forceinline__ void recover(RecIO& io, FilterLds<G>& filt, const ModelArgs ma, const typename Model::Ctx ctx,
+                                        double* wsl, const long wst, const double* lbw, const double* ubw, double* xbuf) {
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2, NP = NX * (NX + 1) / 2;
   const int k = io.k, N = io.N, lane = threadIdx.x & 63;
   const bool valid = io.valid, hasX = io.hasX, hasU = io.hasU, has0 = valid && k == 0;

@@ -22,6 +22,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "collectives.h"
+
 namespace mpcx {
 
 constexpr int NX = 3, NU = 2, NZ = 5, NH = 15;
@@ -115,10 +117,19 @@ __device__ __forceinline__ void uni_value(const StageParams& sp, const double x[
 // weighted moments, accumulated with ~21 FMAs per point, and the gradient and Hessian are
 // assembled from them once per interval (the per-point formula costs ~90).  The value q keeps
 // the per-point sum of the quadratic cost, so the line search's objective is the same expression.
+//
+// RS = 2 (replicated lane groups, kernels.h R = 2): the two replicas of a node -- lanes l and l + 32
+// of the wave, rho = 0 / 1 -- split the RK4 substeps: replica 0 takes the quadrature points of
+// substeps [0, M/2), replica 1 those of [M/2, M) after advancing the rotation and partial sums over
+// the first half without points (the same operations, so its state there has the bits replica 0's
+// would have).  The moments of the two halves are added in one fixed order (lower + upper half, so
+// both replicas hold the same bits) and both take replica 1's end-of-interval partial sums.
+template <int RS = 1>
 __device__ __forceinline__ void uni_derivs_moments(const StageParams& sp, const double x[3], const double u[2],
                                                    const double xr[3], const double ur[2], const double lam[3],
                                                    double fs, double xf[3], double& q, double A[9], double Bm[6],
-                                                   double g[5], double H[15]) {
+                                                   double g[5], double H[15], int rho = 0) {
+  static_assert(RS == 1 || RS == 2, "one or two replicas");
   const double v = u[0], w = u[1], th = x[2];
   const double h = sp.h, hh = 0.5 * h, h6 = h / 6.0, h3 = h / 3.0, third = 1.0 / 3.0;
   const double xix = x[0] - xr[0], xiy = x[1] - xr[1], xit = th - xr[2];
@@ -161,13 +172,14 @@ __device__ __forceinline__ void uni_derivs_moments(const StageParams& sp, const 
     Wt = fma(wt, tau, Wt);
     Wtt = fma(wt * tau, tau, Wtt);
   };
-  for (int m = 0; m < sp.M; ++m) {
+  // one RK4 substep: its quadrature points (pts) and the advance of the rotation and partial sums
+  auto substep = [&](bool pts) __attribute__((always_inline)) {
     const double tm = t0 + hh, te = t0 + h;
     const double c1 = c0 * cd - s0 * sd, s1 = s0 * cd + c0 * sd;
     const double c2 = c1 * cd - s1 * sd, s2 = s1 * cd + c1 * sd;
     const double u1 = hh * c1, v1 = hh * s1, u1t = tm * u1, v1t = tm * v1, u1tt = tm * u1t, v1tt = tm * v1t;
     const double u2 = hh * c2, v2 = hh * s2, u2t = te * u2, v2t = te * v2, u2tt = te * u2t, v2tt = te * v2t;
-    if (sp.cost == 0) {
+    if (pts && sp.cost == 0) {
       // RK4 stage points: (x, th_0), (x + hh f(th_0), th_1), (x + hh f(th_1), th_1), (x + h f(th_1), th_2)
       point(Ac, As, Ac1, As1, Ac2, As2, t0, h6);
       point(Ac + u0, As + v0, Ac1 + u0t, As1 + v0t, Ac2 + u0tt, As2 + v0tt, tm, h3);
@@ -191,6 +203,29 @@ __device__ __forceinline__ void uni_derivs_moments(const StageParams& sp, const 
     u0tt = u2tt;
     v0tt = v2tt;
     t0 = te;
+  };
+  if constexpr (RS == 1) {
+    for (int m = 0; m < sp.M; ++m) substep(true);
+  } else {
+    const int M0 = sp.M / 2;  // replica 0: substeps [0, M0), replica 1: [M0, M)
+    for (int m = 0; m < M0; ++m)
+      if (rho == 1) substep(false);
+    for (int m = 0; m < sp.M - M0; ++m)
+      if (rho == 1 || m < M0) substep(true);
+    // moments: lower + upper half on both replicas; the partial sums: replica 1's (the interval's end)
+    auto sum2 = [](double& s) __attribute__((always_inline)) {
+      const Pair p = halves32(s);
+      s = p.a + p.b;
+    };
+    auto upper = [](double& s) __attribute__((always_inline)) { s = halves32(s).b; };
+    if (sp.cost == 0) {
+      sum2(qs);
+      sum2(Sa); sum2(Sb); sum2(Sa1); sum2(Sb1); sum2(Sa2); sum2(Sb2);
+      sum2(Saa); sum2(Sbb); sum2(Sab); sum2(Saa1); sum2(Sbb1); sum2(Sab1); sum2(Sba1); sum2(Sa1a1);
+      sum2(Sb1b1); sum2(Saa2); sum2(Sbb2);
+      sum2(W0); sum2(Wt); sum2(Wtt);
+    }
+    upper(Ac); upper(As); upper(Ac1); upper(As1); upper(Ac2); upper(As2);
   }
   const double T = sp.T;
   xf[0] = x[0] + v * Ac;

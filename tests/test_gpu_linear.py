@@ -238,8 +238,8 @@ def test_pendulum_decoupled_suffix_same_bits(mpcx, R, N, monkeypatch):
     (solver.hip "decoupled suffix", riccati.h DEC), and later launches start from the P_k an
     earlier one cached.  Same solution bits, multipliers and iteration counts as the full
     recursion (MPCX_DEC_SUFFIX=0), with and without the cache, and the LQ oracle's solution.
-    At N = 100 (two-wave groups) the reused suffix runs as a log-depth vector scan (kernels.h
-    MPCX_DEC_SCAN), whose sums associate differently: there the same iteration counts and a
+    At N = 100 (two-wave groups) the reused suffix runs as a log-depth vector scan (kernels.h,
+    "reused suffix as a log-depth scan"), whose sums associate differently: there the same iteration counts and a
     solution within 1e-9 of the full recursion's."""
     from mpcx import lti
 

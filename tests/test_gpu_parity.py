@@ -309,15 +309,24 @@ def test_horizons(mpcx, C, R, N):
 def test_group_policy_same_results(mpcx, N, B):
     """Lane-group widening (spec.group_policy 0, the default: up to one instance per wave while
     SIMDs would idle) and the narrowest group (policy 1: 4/2 instances per wave at N=10/20) give
-    the same bits: the extra lanes add exact zeros / neutral values to every reduction.  Policy 1
-    is also how the narrow-group code paths stay covered at test batch sizes."""
+    the same results.  Widening a 16-lane group (N = 10) or running one multi-wave group adds exact
+    zeros / neutral values to every reduction: the same bits.  A 32-lane group widened to a wave
+    (N = 20) runs replicated (kernels.h R = 2), and its replicas split the stage evaluation's RK4
+    substeps, summing the quadrature moments in two halves: there the same statuses and iteration
+    counts and a solution within 1e-9 (relative) of the narrow group's.  Policy 1 is also how the
+    narrow-group code paths stay covered at test batch sizes."""
     ocp = mpcx.unicycle_point_to_point(N=N)
     P = config2_batch(B, seed=N + 1)
     r0 = mpcx.nlpsol("s", "mi355x", ocp).solve_batch(P)
     r1 = mpcx.nlpsol("s", "mi355x", ocp, {"group_policy": 1}).solve_batch(P)
     assert np.all(r0["status"] == 0)
+    replicated = 16 <= N < 32
     for n in ("w", "f", "lam_g", "lam_x", "status", "iters"):
-        np.testing.assert_array_equal(r0[n], r1[n], err_msg=n)
+        if replicated and n in ("w", "f", "lam_g", "lam_x"):
+            scale = np.maximum(np.max(np.abs(r1[n]), axis=-1, keepdims=True) if r1[n].ndim > 1 else np.abs(r1[n]), 1.0)
+            assert np.max(np.abs(r0[n] - r1[n]) / scale) <= 1e-9, n
+        else:
+            np.testing.assert_array_equal(r0[n], r1[n], err_msg=n)
 
 
 def test_max_iter_status(mpcx):
@@ -840,10 +849,13 @@ def test_nonfinite_instance_fails_alone(mpcx):
     np.testing.assert_array_equal(r["iters"][others], ref["iters"][others])
 
 
-def test_bench_two_ranks_rehearsal():
+def test_bench_two_ranks_rehearsal(tmp_path):
     """The multi-rank bench path end to end (torch.distributed.run, 2 ranks, weak
     scaling, stats all_gather, max-over-ranks timing), rehearsed on ONE GPU: both ranks on
-    device 0 and gloo collectives (RCCL needs a GPU per rank; the 8-GPU run is the driver's)."""
+    device 0 and gloo collectives (RCCL needs a GPU per rank; the 8-GPU run is the driver's).
+    Sharding is exact: the all-gathered per-instance statistics of the
+    2-rank run -- final states, objective, statuses, iteration counts of every closed-loop
+    step -- equal, bit for bit, those of ONE rank solving the global instance ids [0, 2B)."""
     import json
     import os
     import socket
@@ -858,18 +870,29 @@ def test_bench_two_ranks_rehearsal():
     env = dict(os.environ, MPCX_FORCE_DEVICE="0", MPCX_DIST_BACKEND="gloo")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    flags = ["--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu", "--no-roofline"]
+    B = 512
+    common = ["--steps", "3", "--warmup", "1", "--no-cpu", "--no-roofline", "--no-reference-warm-start"]
+    flags = ["--gpus", "2", "--batch", str(B)] + common
     launched = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py")] + flags
     plain = [sys.executable, os.path.join(ROOT, "bench.py")] + flags  # bench.py starts its 2 ranks itself
-    for cmd in (launched, plain):
-        out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    single = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--batch", str(2 * B)] + common
+    stats = {}
+    for name, cmd in (("launched", launched), ("plain", plain), ("single", single)):
+        dump = str(tmp_path / f"{name}.npy")
+        out = subprocess.run(cmd + ["--dump-stats", dump], env=env if name != "single" else dict(os.environ),
+                             capture_output=True, text=True, timeout=600, cwd=ROOT)
         assert out.returncode == 0, out.stderr[-3000:]
         lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
         assert len(lines) == 1  # rank 0 prints ONE line
         d = json.loads(lines[0])
-        assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * d["config"]["batch_per_gpu"]
+        n = 1 if name == "single" else 2
+        assert d["n_gpus"] == n and d["config"]["global_batch"] == n * d["config"]["batch_per_gpu"] == 2 * B
         assert d["failed_instances"] == 0 and d["value"] > 0 and d["steps"] == 3
+        stats[name] = np.load(dump)
+    assert stats["single"].shape == (2 * B, 8)
+    for name in ("launched", "plain"):
+        np.testing.assert_array_equal(stats[name], stats["single"], err_msg=name)
 
 
 def test_mpctools_variant_closed_loop_3exemplo(mpcx, R, golden):

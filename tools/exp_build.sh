@@ -2,7 +2,7 @@
 # Experiment build: recompile ONE model unit with extra flags and link it with the other units'
 # current objects into mpc-verde_amd/mpcx/libmpcx_<tag>.so (load it with MPCX_LIB=... and
 # MPCX_ALLOW_STALE_LIB=1).  A/B of compile-time switches without a full rebuild.
-#   tools/exp_build.sh TAG UNIT [hipcc flags...]     e.g. tools/exp_build.sh nores unicycle -DMPCX_UNICYCLE_RESTO=false
+#   tools/exp_build.sh TAG UNIT [hipcc flags...]     e.g. tools/exp_build.sh ev unicycle_xfree -DMPCX_STAMP_EVAL
 #   EXP_BASE=build/stamps tools/exp_build.sh st unicycle -DMPCX_STAMPS ...   (diagnostic-build variant)
 set -euo pipefail
 TAG=$1; UNIT=$2; shift 2
