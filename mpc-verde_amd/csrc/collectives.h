@@ -123,6 +123,53 @@ __device__ __forceinline__ double greduce(double v, XWave<G>& xw) {
   }
   return v;
 }
+// Several group reductions at once (OPS: 0 sum, 1 max, 2 min, one per value): the in-wave DPP
+// chains as greduce's, and for groups wider than a wave ONE LDS exchange and barrier for all of
+// them (a barrier is the expensive part there: the waves of a group meet at every one).
+__device__ __forceinline__ double op_apply(int op, double a, double b) {  // op a compile-time constant after unrolling
+  return op == 0 ? a + b : op == 1 ? qmax(a, b) : qmin(a, b);
+}
+template <int G>
+__device__ __forceinline__ double wreduce(int op, double v) {  // over the group's lanes inside one wave
+  v = op_apply(op, v, dpp<kQuadXor1>(v));
+  v = op_apply(op, v, dpp<kQuadXor2>(v));
+  v = op_apply(op, v, dpp<kHalfMirror>(v));
+  v = op_apply(op, v, dpp<kMirror>(v));
+  if (G >= 32) {
+    const Pair p = rows16(v);
+    v = op_apply(op, p.a, p.b);
+  }
+  if (G >= 64) {
+    const Pair p = halves32(v);
+    v = op_apply(op, p.a, p.b);
+  }
+  return v;
+}
+template <int G, int... OPS>
+__device__ __forceinline__ void greduce_n(double* v, XWave<G>& xw) {
+  constexpr int n = sizeof...(OPS);
+  constexpr int ops[n] = {OPS...};
+  static_assert(n <= kXchStride, "exchange slot");
+#pragma unroll
+  for (int i = 0; i < n; ++i) v[i] = wreduce<G>(ops[i], v[i]);
+  if constexpr (G > 64) {
+    constexpr int W = G / 64;
+    double* b = xw.cur();
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+      for (int i = 0; i < n; ++i) b[(threadIdx.x >> 6) * kXchStride + i] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      double r = b[i];
+#pragma unroll
+      for (int w = 1; w < W; ++w) r = op_apply(ops[i], r, b[w * kXchStride + i]);  // same order on every wave
+      v[i] = r;
+    }
+    xw.slot ^= 1;
+  }
+}
+
 template <int G>
 __device__ __forceinline__ double gsum(double v, XWave<G>& xw) {
   return greduce<G, OpSum>(v, xw);

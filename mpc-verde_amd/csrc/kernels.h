@@ -259,9 +259,10 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   __shared__ double sbuf[Model::kParallelRiccati ? RElem<NX>::NE * kSBS : 1];
   // LDS cache of the ODE models' transcendental values across their derivative passes (ode.h)
   __shared__ double tcache[Model::kTrigSlots > 0 ? Model::kTrigSlots * kSBS : 1];
-  // the decoupled suffix's vector scan (multi-wave groups): NX doubles per thread, then the
-  // matrix powers (A^T)^(2^l), l < 8
-  __shared__ double dscan[DecSuffixOf<Model>::value && G > 64 ? NX * kSBS + 8 * NX * NX : 1];
+  // the decoupled suffix's vector scan (multi-wave groups): two NX-double buffers per thread, then
+  // the matrix powers (A^T)^(j 4^l), j = 1..3, l < 5, kept for the launch (table index pow_tab)
+  __shared__ double dscan[DecSuffixOf<Model>::value && G > 64 ? 2 * NX * kSBS + 15 * NX * NX : 1];
+  double pow_tab = -1.0;  // table whose powers dscan holds (block-uniform)
   // workspace chain stash (solver.h chain_ws_slots): slots after the restoration workspace's
   constexpr bool kWsStash = WsStashOf<Model>::value;
   // The stash is one contiguous record per thread (array of structures, after the restoration
@@ -355,6 +356,18 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     if constexpr (kBndLds) {
       lb.relaunder();
       ub.relaunder();
+    }
+  };
+  // two group tests at once: ballots in a wave, one exchange for groups wider than a wave
+  auto group_tests2 = [&](bool c0_, bool c1_, bool& r0, bool& r1) __attribute__((always_inline)) {
+    if constexpr (G > 64) {
+      double t[2] = {c0_ ? 1.0 : 0.0, c1_ ? 1.0 : 0.0};
+      greduce_n<G, 2, 2>(t, xw);
+      r0 = t[0] > 0.5;
+      r1 = t[1] > 0.5;
+    } else {
+      r0 = gall<G, G * R>(c0_, xw);
+      r1 = gall<G, G * R>(c1_, xw);
     }
   };
   const double nbound = gsum<G>((double)nbnd_l, xw);
@@ -882,8 +895,10 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     // holds iff it holds on every lane (gall: one ballot instead of a max reduction each; max is
     // exact and the division by a positive group-uniform scaling monotone, so the decisions are the
     // ones the reduced values give)
-    lam1 = gsum<G>(lam1, xw);
-    z1 = gsum<G>(z1, xw);
+    double sums[3] = {lam1, z1, hasU ? qv : 0.0};  // one exchange for the three group sums
+    greduce_n<G, 0, 0, 0>(sums, xw);
+    lam1 = sums[0];
+    z1 = sums[1];
     // IPOPT's scalings s_d = max(s_max, (|lam|_1 + |z|_1) / (m + n)) / s_max and s_c = max(s_max,
     // |z|_1 / n_b) / s_max are exactly 1 unless the sum exceeds s_max times the count (a rounded
     // quotient that reaches s_max from above still gives 1): the IEEE divisions -- group-uniform
@@ -906,13 +921,14 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     // constraint violation and complementarity tests; then the acceptable level (all of
     // acceptable_* and the objective change from the previous iterate) for acceptable_iter
     // iterates in a row.  fcur = the scaled objective.
-    const double fcur = fs * gsum<G>(hasU ? qv : 0.0, xw);
-    const bool acceptable_now =
-        gall<G, G * R>(E0 <= a.acc_tol && Ed <= a.acc_dual_inf_tol * fs && Ec <= a.acc_constr_viol_tol &&
-                       Ecomp0 <= a.acc_compl_inf_tol * fs, xw) &&
-        fabs(fcur - f_last) <= a.acc_obj_change_tol * fmax(1.0, fabs(fcur));
-    if (gall<G, G * R>(E0 <= a.tol && Ed <= a.dual_inf_tol * fs && Ec <= a.constr_viol_tol &&
-                       Ecomp0 <= a.compl_inf_tol * fs, xw) && !done) {
+    const double fcur = fs * sums[2];
+    bool conv_g, acc_g;
+    group_tests2(E0 <= a.tol && Ed <= a.dual_inf_tol * fs && Ec <= a.constr_viol_tol && Ecomp0 <= a.compl_inf_tol * fs,
+                 E0 <= a.acc_tol && Ed <= a.acc_dual_inf_tol * fs && Ec <= a.acc_constr_viol_tol &&
+                     Ecomp0 <= a.acc_compl_inf_tol * fs,
+                 conv_g, acc_g);
+    const bool acceptable_now = acc_g && fabs(fcur - f_last) <= a.acc_obj_change_tol * fmax(1.0, fabs(fcur));
+    if (conv_g && !done) {
       done = true;
       status = 0;
       its = it;
@@ -1110,7 +1126,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
         }
         // scan usable: stage R positive definite, finite, and consistent with the step
         const bool good = eok && dev <= 1e-8 * mag;  // false for NaN
-        seq = gmin<G>(good ? 1.0 : 0.0, xw) < 0.5;
+        seq = !gall<G, G * R>(good, xw);
         DIAG_IF(seq && !done, 8);
       }
       // Stash: the iterate, its bound multipliers, bounds and lam are live across the sequential
@@ -1179,32 +1195,47 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
         // The reused suffix as a log-depth scan (multi-wave groups: one instance per block).  On
         // a reused stage p_k = A^T p_{k+1} + r_k with r_k = gp_x + A^T (P_{k+1} c), and when every
         // stage of the suffix uses the same table (shared tables) the composition of d steps is
-        // the uniform (A^T)^d: a Hillis-Steele suffix scan v_k += (A^T)^d v_{k+d} carries only the
-        // NX-vector, the powers (A^T)^(2^l) formed once per factorisation by NX^2 threads in LDS.
-        // log2(N) levels replace the suffix's N - jc dependent steps (config 5: 95 of 100).
+        // the uniform (A^T)^d: a radix-4 Hillis-Steele suffix scan
+        //   v_k += (A^T)^d v_{k+d} + (A^T)^{2d} v_{k+2d} + (A^T)^{3d} v_{k+3d},   d = 1, 4, 16, 64
+        // carries only the NX-vector through ping-pong LDS buffers, ONE barrier per level (config 5:
+        // 4 levels replace the suffix's 95 dependent steps; a radix-2 scan needs 7 levels of two
+        // barriers).  The powers (A^T)^(j 4^l) depend only on the table: they are formed by NX^2
+        // threads in LDS the first time a launch scans a table and kept there for the launch.
         bool sscan = false;  // group-uniform
         if constexpr (kDec && G > 64) {
           if (jc < N && !a.lin.per_instance && a.tabseq == nullptr) {
             const bool mine = k >= jc && k < N;
             const double ti = (double)((ctx.A - a.lin.A) / (NX * NX));  // my stage's table
-            const double tmax = gmax<G>(mine ? ti : -1.0, xw), tmin = gmin<G>(mine ? ti : 1e300, xw);
-            sscan = tmin == tmax;
+            double tt[2] = {mine ? ti : -1.0, mine ? ti : 1e300};
+            greduce_n<G, 1, 2>(tt, xw);
+            const double tmax = tt[0];
+            sscan = tt[1] == tmax;
             if (sscan) {
-              const double* Au = a.lin.A + (size_t)tmax * NX * NX;
-              double* mpow = dscan + NX * kSBS;  // level l: (A^T)^(2^l), row-major
+              double* mpow = dscan + 2 * NX * kSBS;  // (A^T)^(j 4^l) at mpow[(3 l + j - 1) NX^2], row-major
               const int t = (int)threadIdx.x;
-              if (t < NX * NX) mpow[t] = Au[(t % NX) * NX + t / NX];
-              __syncthreads();
-              for (int l = 1; (1 << l) < G && (1 << l) <= N; ++l) {
-                if (t < NX * NX) {
-                  const double* Mp = mpow + (l - 1) * NX * NX;
-                  const int i = t / NX, j = t % NX;
-                  double acc = Mp[i * NX] * Mp[j];
+              constexpr int kLev = G > 64 ? (G <= 256 ? 4 : 5) : 1;  // 4^kLev >= G
+              if (tmax != pow_tab) {  // block-uniform
+                const double* Au = a.lin.A + (size_t)tmax * NX * NX;
+                auto mul = [&](int dst, int x, int y) __attribute__((always_inline)) {  // mpow[dst] = X Y
+                  if (t < NX * NX) {
+                    const double* X = mpow + x * NX * NX;
+                    const double* Y = mpow + y * NX * NX;
+                    const int i = t / NX, j = t % NX;
+                    double acc = X[i * NX] * Y[j];
 #pragma unroll
-                  for (int m = 1; m < NX; ++m) acc = fma(Mp[i * NX + m], Mp[m * NX + j], acc);
-                  mpow[l * NX * NX + t] = acc;
-                }
+                    for (int m = 1; m < NX; ++m) acc = fma(X[i * NX + m], Y[m * NX + j], acc);
+                    mpow[dst * NX * NX + t] = acc;
+                  }
+                  __syncthreads();
+                };
+                if (t < NX * NX) mpow[t] = Au[(t % NX) * NX + t / NX];
                 __syncthreads();
+                for (int l = 0; l < kLev; ++l) {
+                  if (l > 0) mul(3 * l, 3 * l - 2, 3 * l - 2);  // (A^T)^(4^l) = ((A^T)^(2 4^(l-1)))^2
+                  mul(3 * l + 1, 3 * l, 3 * l);                 // (A^T)^(2 4^l)
+                  mul(3 * l + 2, 3 * l + 1, 3 * l);             // (A^T)^(3 4^l)
+                }
+                pow_tab = tmax;
               }
               double v[NX];
 #pragma unroll
@@ -1215,23 +1246,31 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
                   if (Model::AMASK & (1ull << (m * NX + i))) acc = fma(Aop[m * NX + i], vpc[m], acc);
                 v[i] = mine ? acc : (k == N ? p[i] : 0.0);
               }
-              for (int d = 1, l = 0; d < G && d <= N; d <<= 1, ++l) {
+              double* buf = dscan;  // ping-pong: level l reads buf[l % 2], writes buf[(l + 1) % 2]
 #pragma unroll
-                for (int i = 0; i < NX; ++i) dscan[i * kSBS + t] = v[i];
-                __syncthreads();
-                if (t + d < G) {
-                  const double* M = mpow + l * NX * NX;
-                  double w[NX];
+              for (int i = 0; i < NX; ++i) buf[i * kSBS + t] = v[i];
+              __syncthreads();
+              for (int l = 0, d = 1; l < kLev && d <= N; ++l, d *= 4) {
+                const double* cur = dscan + (l & 1) * NX * kSBS;
+                double* nxt = dscan + ((l + 1) & 1) * NX * kSBS;
 #pragma unroll
-                  for (int i = 0; i < NX; ++i) w[i] = dscan[i * kSBS + t + d];
+                for (int q = 1; q <= 3; ++q) {
+                  if (t + q * d < G) {
+                    const double* M = mpow + (3 * l + q - 1) * NX * NX;
+                    double w[NX];
 #pragma unroll
-                  for (int i = 0; i < NX; ++i) {
-                    double acc = v[i];
+                    for (int i = 0; i < NX; ++i) w[i] = cur[i * kSBS + t + q * d];
 #pragma unroll
-                    for (int j = 0; j < NX; ++j) acc = fma(M[i * NX + j], w[j], acc);
-                    v[i] = acc;
+                    for (int i = 0; i < NX; ++i) {
+                      double acc = v[i];
+#pragma unroll
+                      for (int j = 0; j < NX; ++j) acc = fma(M[i * NX + j], w[j], acc);
+                      v[i] = acc;
+                    }
                   }
                 }
+#pragma unroll
+                for (int i = 0; i < NX; ++i) nxt[i * kSBS + t] = v[i];
                 __syncthreads();
               }
               if (seq && mine) {
@@ -1626,12 +1665,20 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
       tiny_l = qmax(tiny_l, own ? fma(-10.0 * kEps, 1.0 + fabs(z[i]), fabs(dz[i])) : -1.0);
       if (own) gd_l += gp[i] * dz[i];
     }
-    const double amax = gmin<G>(amax_l, xw);
-    double az = gmin<G>(az_l, xw);  // dual step length (a second-order correction replaces it)
-    const bool tinystep = gall<G, G * R>(tiny_l < 0.0, xw);  // max over the group < 0
+    // amax, az (min), gd (sum) and the tiny-step test (max over the group < 0) in one exchange
+    double fr[4] = {amax_l, az_l, gd_l, tiny_l < 0.0 ? 1.0 : 0.0};
+    if constexpr (G > 64) {
+      greduce_n<G, 2, 2, 0, 2>(fr, xw);
+    } else {
+      greduce_n<G, 2, 2, 0>(fr, xw);
+      fr[3] = gall<G, G * R>(tiny_l < 0.0, xw) ? 1.0 : 0.0;
+    }
+    const double amax = fr[0];
+    double az = fr[1];  // dual step length (a second-order correction replaces it)
+    const bool tinystep = fr[3] > 0.5;
     if (!done && amax < 1.0) DIAG(4);
     if (!done && tinystep) DIAG(5);
-    const double gd = gsum<G>(gd_l, xw);
+    const double gd = fr[2];
 
     STAMP(6);
     phase();
@@ -1639,7 +1686,9 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     double thk_l = 0, phk_l = (hasU ? fs * qv : 0.0) - mu * barrier_logsum<NZ>(z, lb, ub, hL, hU);
 #pragma unroll
     for (int i = 0; i < NX; ++i) thk_l += fabs(cdef[i]) + fabs(c0[i]);
-    const double thk = gsum<G>(thk_l, xw), phk = gsum<G>(phk_l, xw);
+    double tp[2] = {thk_l, phk_l};
+    greduce_n<G, 0, 0>(tp, xw);
+    const double thk = tp[0], phk = tp[1];
     double alpha = amax;
     bool searching = !done && !tinystep && !(kRes && soft);
     bool accepted = !done && tinystep;
@@ -1696,7 +1745,9 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
           for (int i = 0; i < NX; ++i) tht_l += fabs(x0[i] - zt[i]);
       }
       pht_l -= mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU);
-      const double tht = gsum<G>(tht_l, xw), pht = gsum<G>(pht_l, xw);
+      double tp_[2] = {tht_l, pht_l};
+      greduce_n<G, 0, 0>(tp_, xw);
+      const double tht = tp_[0], pht = tp_[1];
       const bool infilter = filt.contains(tht, pht, xw);
       if (searching) {
         // sufficient decrease (switching condition + Armijo, or theta/phi decrease), then the
@@ -1878,8 +1929,10 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
 #pragma unroll
         for (int i = 0; i < NX; ++i) tht_l += fabs(ct0[i]);
       pht_l -= mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU);
-      tht = gsum<G>(tht_l, xw);
-      pht = gsum<G>(pht_l, xw);
+      double tp_[2] = {tht_l, pht_l};
+      greduce_n<G, 0, 0>(tp_, xw);
+      tht = tp_[0];
+      pht = tp_[1];
       infilter = filt.contains(tht, pht, xw);
     };
     // acceptance of a trial point for step length al (W&B 2006 A-5.4): sufficient decrease

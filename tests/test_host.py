@@ -184,6 +184,11 @@ def test_bench_group_size_and_usable_cpus():
             for pol in (0, 1):
                 assert bench.group_size(N, B, 1024, pol) == cpp_rule(N, B, 1024, pol)
     assert bench.group_size(20, 1024, 1024) == 64 and bench.group_size(30, 4096, 1024) == 32
+    # kernels.h launch_solve_model: a 32-lane group widened to a wave runs replicated (unicycle)
+    assert bench.kernel_group("UnicycleFreeModel", 20, 1024, 1024) == (32, 2)
+    assert bench.kernel_group("UnicycleFreeModel", 20, 1024, 1024, 1) == (32, 1)
+    assert bench.kernel_group("UnicycleScanModel", 30, 1024, 1024) == (64, 1)
+    assert bench.kernel_group("LinearModel<5, 1>", 100, 2048, 1024) == (128, 1)
     old = os.environ.get("OMP_NUM_THREADS")
     os.environ["OMP_NUM_THREADS"] = "1"
     try:
@@ -210,7 +215,7 @@ def test_bench_solve_roofline_uses_only_a_current_pmc_record(tmp_path, monkeypat
     spec.loader.exec_module(bench)
     from mpcx import _lib
 
-    kname = "void mpcx::solve_kernel<mpcx::UnicycleFreeModel, 64, false>(mpcx::SolveArgs)"
+    kname = "void mpcx::solve_kernel<mpcx::UnicycleFreeModel, 32, false, 2>(mpcx::SolveArgs)"
     rec = {kname: {"f64_lane_flops_per_group_iteration": 400000.0,
                    "wave_cycles_share": {"issuing": 0.8, "dependency_or_pipe_stall": 0.02, "waitcnt_or_barrier": 0.18},
                    "valu_active_share": 0.7}}
@@ -221,7 +226,7 @@ def test_bench_solve_roofline_uses_only_a_current_pmc_record(tmp_path, monkeypat
         meta = {"mpcx_source_hash": _lib.source_hash() if current else "0000000000000000"}
         with open(tmp_path / bench.SOLVE_PMC, "w") as f:
             json.dump({"_meta": meta, **rec}, f)
-        r = bench.solve_roofline("UnicycleFreeModel", 64, algo, 100000, 2.0)  # 4e9 flops in 2 ms
+        r = bench.solve_roofline("UnicycleFreeModel", 32, algo, 100000, 2.0, R=2)  # 4e9 flops in 2 ms
         assert r["achieved"] == pytest.approx(2.0) and r["frac"] == pytest.approx(2.0 / bench.PEAK_FP64_TFLOPS, abs=1e-5)
         if current:
             assert r["issued"]["algorithmic_over_issued"] == pytest.approx(0.1)

@@ -88,7 +88,11 @@ def summarise(root):
              "f64_insts_per_dispatch": f64, "f64_lane_flops_per_dispatch": flops,
              "valu_f64_share_of_valu": round(sum(f64.values()) / max(ca["SQ_INSTS_VALU"], 1.0), 4),
              "group_iterations_in_run": its,
-             "f64_lane_flops_per_group_iteration": (flops_total / its) if its and ", true>" not in k else None}
+             "f64_lane_flops_per_group_iteration": (flops_total / its) if its and ", true," not in k else None,
+             # wave-level VALU instructions per IPM iteration of one instance (one wave per instance
+             # for groups of 64 lanes or replicated 32-lane groups; G < 64 groups share a wave)
+             "valu_insts_per_group_iteration": (ca["_total"]["SQ_INSTS_VALU"] / its) if its and ", true," not in k
+             else None}
         if t:
             r["fp64_tflops"] = round(flops / t / 1e12, 3)
             r["fp64_frac_of_peak"] = round(flops / t / 1e12 / PEAK_FP64_TFLOPS, 4)
