@@ -37,6 +37,7 @@
 // accounting of the solve loop (cdna_hip_programming.md §7 "In-kernel stamps").
 #ifdef MPCX_STAMPS
 static __device__ unsigned long long* g_mpcx_stamps = nullptr;
+constexpr int kStampSlots = 16;  // per wave: phases 0-9, sub-phases 10-15 (-DMPCX_STAMP_SUB)
 // per-instance event counters (diagnostic build; indices at the kernel's `diag` array)
 static __device__ int* g_mpcx_diag = nullptr;
 constexpr int kDiag = 15;  // counters per instance
@@ -59,6 +60,16 @@ constexpr int kDiag = 15;  // counters per instance
 #define STAMP(p) \
   do {           \
   } while (0)
+#endif
+// finer split of the errors and Riccati phases (diagnostic build with -DMPCX_STAMP_SUB)
+#if defined(MPCX_STAMPS) && defined(MPCX_STAMP_SUB)
+#define STAMP_SUB(p) STAMP(p)
+#else
+#define STAMP_SUB(p) \
+  do {               \
+  } while (0)
+#endif
+#ifndef MPCX_STAMPS
 #define DIAG(i) \
   do {          \
   } while (0)
@@ -558,7 +569,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   // calls, resto.h), 13 restoration-phase iterations, 14 filter additions that found all G
   // slots holding mutually non-dominated entries (filter_add; an entry was overwritten)
   int diag[kDiag] = {};
-  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_acc[kStampSlots] = {};
   unsigned long long st_last = 0;
   int st_ph = 9;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
@@ -896,7 +907,9 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     // exact and the division by a positive group-uniform scaling monotone, so the decisions are the
     // ones the reduced values give)
     double sums[3] = {lam1, z1, hasU ? qv : 0.0};  // one exchange for the three group sums
+    STAMP_SUB(14);
     greduce_n<G, 0, 0, 0>(sums, xw);
+    STAMP_SUB(15);
     lam1 = sums[0];
     z1 = sums[1];
     // IPOPT's scalings s_d = max(s_max, (|lam|_1 + |z|_1) / (m + n)) / s_max and s_c = max(s_max,
@@ -1040,6 +1053,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     Fac<NX, NU> fac = {};
     for (int attempt = 0; attempt < 64; ++attempt) {
       if (!__any(need)) break;
+      STAMP_SUB(10);
       // node-parallel: stage Hessian + Sigma + delta (off the sequential path)
       double Hd[NH], sgv[NZ];
       // stage Hessian (table-Hessian models: 2 fs W of the stage table; none at node N)
@@ -1201,6 +1215,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
         // 4 levels replace the suffix's 95 dependent steps; a radix-2 scan needs 7 levels of two
         // barriers).  The powers (A^T)^(j 4^l) depend only on the table: they are formed by NX^2
         // threads in LDS the first time a launch scans a table and kept there for the launch.
+        STAMP_SUB(11);
         bool sscan = false;  // group-uniform
         if constexpr (kDec && G > 64) {
           if (jc < N && !a.lin.per_instance && a.tabseq == nullptr) {
@@ -1283,6 +1298,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
             }
           }
         }
+        STAMP_SUB(12);
         if constexpr (G <= 64) {
           if constexpr (kDec) {
             for (int j = N - 1; j >= jc; --j) {
@@ -1414,6 +1430,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
           }
         }
       }
+      STAMP_SUB(13);
       stash(true);
       // node 0: A_0 = 0 and no x blocks in stage 0 (interval 0 integrates from x0), so the step
       // gives P_0 = Sigma_x + delta and p_0 = the barrier gradient, as at node N; its factors
@@ -2304,7 +2321,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     for (int i = 0; i < kDiag; ++i) g_mpcx_diag[(size_t)inst * kDiag + i] = diag[i];
   if (g_mpcx_stamps && !RESUME && (threadIdx.x & 63) == 0) {
     const long wv = gid / 64;
-    for (int i = 0; i < 10; ++i) g_mpcx_stamps[wv * 10 + i] = st_acc[i];
+    for (int i = 0; i < kStampSlots; ++i) g_mpcx_stamps[wv * kStampSlots + i] = st_acc[i];
   }
 #endif
 

@@ -26,7 +26,12 @@ from mpcx import dist  # noqa: E402
 from mpcx.device import DeviceLoop  # noqa: E402
 
 PHASES = ["errors", "barrier_update", "sigma", "riccati", "forward", "fraction", "linesearch", "update", "sweep",
-          "exit"]
+          "exit",
+          # sub-phases of a -DMPCX_STAMP_SUB build (0 otherwise): the Riccati phase's node-parallel
+          # stage setup, reused-suffix scan, sequential chain and post-chain part; the errors
+          # phase's group sums and its tests
+          "ric_stage", "ric_scan", "ric_chain", "ric_post", "err_sums", "err_tests"]
+SLOTS = 16  # kernels.h kStampSlots
 
 
 def main():
@@ -65,11 +70,11 @@ def main():
     while G < 64 and a.batch * G * 2 <= 64 * n_simd:  # launch_solve_model's widening rule
         G *= 2
     waves = (a.batch * G + 63) // 64
-    buf = torch.zeros(waves * 10, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(waves * SLOTS, dtype=torch.int64, device="cuda")
     assert lib.mpcx_diag_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
     loop.solve()
     torch.cuda.synchronize()
-    acc = buf.view(waves, 10).cpu().numpy().astype(float)
+    acc = buf.view(waves, SLOTS).cpu().numpy().astype(float)
     it_inst = loop.iters.cpu().numpy()
     iters = np.array([it_inst[(w * 64) // G] if G >= 64 else it_inst[w * (64 // G):(w + 1) * (64 // G)].max()
                       for w in range(waves)])
@@ -79,6 +84,10 @@ def main():
            "cycles_per_iter": tot / max(iters[slow], 1),
            "share": {p: round(acc[slow, i] / tot, 4) for i, p in enumerate(PHASES)},
            "share_all_waves": {p: round(acc[:, i].sum() / acc.sum(), 4) for i, p in enumerate(PHASES)}}
+    if G > 64:  # multi-wave groups: each wave of the slowest wave's group, cycles per IPM iteration
+        w0 = slow - slow % (G // 64)
+        out["group_waves_cycles_per_iter"] = [
+            {p: round(acc[w, i] / max(iters[slow], 1)) for i, p in enumerate(PHASES)} for w in range(w0, w0 + G // 64)]
     print(json.dumps(out, indent=1))
 
 
