@@ -19,7 +19,7 @@ max-over-ranks wall time per step; ms_per_solve_p50 = median batched solve-call
 latency (HIP events).  `roofline` describes the kernel that dominates the timed
 region, the fused solve_kernel: algorithmic FP64 flops per launch (the flops one
 IPM iteration of one instance needs -- per-node evaluation and Riccati step
-measured by tools/flop_probe.py, profiles/r03_flop_probe.json, plus the IPM's
+measured by tools/flop_probe.py, profiles/r04_flop_probe.json, plus the IPM's
 vector work counted in ipm_vector_flops; DESIGN.md §6 -- x the launch's
 instance-iterations) / the launch's HIP-event time / the FP64 vector peak, with
 the issued FP64 lane-flops of profiles/r03_solve_kernel_pmc.json beside it while
@@ -270,12 +270,12 @@ def usable_cpus():
 # ---- algorithmic FP64 work of one IPM iteration of one instance
 # Per node with an interval: one stage evaluation E (Model::derivs) + one backward Riccati
 # step R (riccati_step + riccati_gains), both measured per unit on the device by
-# tools/flop_probe.py (profiles/r03_flop_probe.json), + the IPM's vector work V below, counted
+# tools/flop_probe.py (profiles/r04_flop_probe.json), + the IPM's vector work V below, counted
 # from the sequential algorithm (the log-depth scans' extra compositions, group-uniform
 # recomputation on every lane, padding lanes and the line search's further trials are not
 # algorithmic work and are not counted).  Linear models' E is counted analytically (their
 # Jacobians and Hessians are tables).
-FLOP_PROBE = os.path.join("profiles", "r03_flop_probe.json")
+FLOP_PROBE = os.path.join("profiles", "r04_flop_probe.json")
 ALGO_KEYS = {  # workload -> (eval key or None for a linear model, riccati key)
     2: ("unicycle_quadrature_M4", "unicycle"), 3: ("unicycle_node_M1", "unicycle"),
     4: (None, "linear4x1"), 5: (None, "linear5x1"),

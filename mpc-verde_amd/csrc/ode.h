@@ -1,4 +1,5 @@
-// ode.h -- nonlinear ODE stage models with exact derivatives by second-order forward mode.
+// ode.h -- nonlinear ODE stage models with exact derivatives (second-order forward mode, or
+// forward sensitivities with stage adjoints).
 //
 // The BASELINE configs name three nonlinear models that the reference only has in linearised
 // or renamed form.  Each is written once, templated on its scalar
@@ -15,7 +16,9 @@
 //                phi = 0 is exactly the reference's Ac, Bc with M = m = 1, L = 0.5, c = 10
 //                (Inverted_pendulum/inverted_pendulum_single_shooting_mpctools.py:19-23).
 //
-// Derivatives.  A hyper-dual number v + a e1 + b e2 + ab e1e2 (e1^2 = e2^2 = 0) carries the
+// Derivatives.  The 6-state bicycle: forward sensitivities and stage adjoints through RK4 with
+// closed-form partials of f (OdeModel::derivs_adjoint, below).  The others, and the 6-state
+// model's reference path: a hyper-dual number v + a e1 + b e2 + ab e1e2 (e1^2 = e2^2 = 0) carries the
 // first derivatives along two seed directions and the mixed second derivative.  One RK4 pass
 // seeded with (e_i, e_j) gives columns i and j of dF/dz and d2F/dz_i dz_j exactly (no
 // truncation).  Passes run over the pairs of variables whose second derivatives through the RK4
@@ -92,6 +95,8 @@ struct TrigDirect {
   __device__ __forceinline__ HD recip_x(HD x) { return recip(x); }
   __device__ __forceinline__ HD div_x(HD n, HD d) { return n / d; }
   __device__ __forceinline__ HD tan_u(HD x) { return tan(x); }
+  template <int NX, class S>
+  __device__ __forceinline__ void substep(int, const S*) {}
 };
 // slots: [0, 2) input-only (sincos_u or tan_u), then per stage evaluation in call order
 struct TrigRecord {
@@ -123,6 +128,8 @@ struct TrigRecord {
     buf[0] = t;
     return t;
   }
+  template <int NX, class S>
+  __device__ __forceinline__ void substep(int, const S*) {}
 };
 struct TrigReplay {
   const double* buf;
@@ -146,6 +153,40 @@ struct TrigReplay {
     const double t = buf[0], d = fma(t, t, 1.0);
     return {t, d * x.a, d * x.b, fma(d, x.ab, 2.0 * t * d * x.a * x.b)};
   }
+  template <int NX, class S>
+  __device__ __forceinline__ void substep(int, const S*) {}
+};
+// The adjoint derivative path's evaluations (OdeModel::derivs_adjoint): transcendental values
+// computed directly, as TrigDirect (so a value pass gives value()'s bits), with sincos of the
+// input-only argument taken once per interval, the last f call's sincos(x) and reciprocal kept
+// for its partials, and the state at each RK4 substep start stored to this lane's LDS column
+// (checkpoints of the reverse pass)
+struct TrigAdj {
+  double* ck;  // checkpoint slot 0 (slot i at ck[i * stride]) or nullptr
+  int stride;
+  double su, cu;       // sincos of the input-only argument
+  double sx, cx, rx;   // the last call's sincos_x and recip_x values
+  __device__ __forceinline__ void sincos_x(double x, double& s, double& c) {
+    ::sincos(x, &s, &c);
+    sx = s;
+    cx = c;
+  }
+  __device__ __forceinline__ void sincos_u(double, double& s, double& c) {
+    s = su;
+    c = cu;
+  }
+  __device__ __forceinline__ double recip_x(double x) {
+    rx = 1.0 / x;
+    return rx;
+  }
+  __device__ __forceinline__ double div_x(double n, double d) { return n / d; }
+  __device__ __forceinline__ double tan_u(double x) { return ::tan(x); }
+  template <int NX, class S>
+  __device__ __forceinline__ void substep(int s, const S* x) {
+    if (ck)
+#pragma unroll
+      for (int i = 0; i < NX; ++i) ck[(NX * s + i) * stride] = x[i];
+  }
 };
 
 // ---------------------------------------------------------------------------- dynamics
@@ -155,6 +196,7 @@ struct KinBicycle {
   static constexpr unsigned NLMASK = (1u << 2) | (1u << 3) | (1u << 4);  // psi, v, delta
   static constexpr unsigned INDEP = (1u << 0) | (1u << 1);               // f does not read X, Y
   static constexpr int kTrigPerEval = 2, kTrigInput = 1, kTrigMaxM = 1;  // sincos(psi); tan(delta)
+  static constexpr bool kAdjoint = false;  // derivatives by hyper-dual passes (OdeModel::derivs)
   template <class S, class Tc>
   __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx, Tc& tc) {
     S sp, cp;
@@ -173,6 +215,10 @@ struct DynBicycle {
   static constexpr unsigned NLMASK = (1u << 2) | (1u << 3) | (1u << 4) | (1u << 5) | (1u << 6) | (1u << 7);
   static constexpr unsigned INDEP = (1u << 0) | (1u << 1);
   static constexpr int kTrigPerEval = 3, kTrigInput = 2, kTrigMaxM = 4;  // sincos(psi), 1/vx; sincos(delta)
+  // closed-form partials below (OdeModel::derivs_adjoint).  A/B on one MI355X (config 4 lane
+  // change, N = 50, alternating builds): 459-476 -> 258-261 us per IPM iteration, 136 k -> 337 k
+  // solves/s in 10-step launches, lock-step 85 k -> 125 k, against the hyper-dual passes
+  static constexpr bool kAdjoint = true;
   template <class S, class Tc>
   __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx, Tc& tc) {
     // par = (m, a, b, Ca, Jz): Trajectory_tracking_dynamic_model.py:36-40 (a, b = CG-axle distances)
@@ -191,6 +237,105 @@ struct DynBicycle {
     dx[4] = (Fyf * cd + Fyr) * (1.0 / m) - vx * r;
     dx[5] = (a * (Fyf * cd) - b * Fyr) * (1.0 / Jz);
   }
+
+  // ---- closed-form partials for the adjoint derivatives (OdeModel::derivs_adjoint).  f reads
+  // the states psi, vx, vy, r (x[2..5]) and both inputs; v = (psi, vx, vy, r, delta, ax) below.
+  // With w = 1/vx, P1 = vy + a r, P2 = vy - b r, C = 2 Ca:
+  //   Fyf = C (delta - P1 w),  Fyr = -C P2 w,
+  // and for an adjoint mu of f's value, mu^T f = mu0 f0 + mu1 f1 + mu2 r + mu3 (ax + r vy)
+  // - mu4 vx r + Fyf al(delta) + Fyr be, with
+  //   al = -mu3 sin(delta) / m + (mu4 / m + mu5 a / Jz) cos(delta),  be = mu4 / m - mu5 b / Jz,
+  // so its gradient and Hessian follow from those of Fyf and Fyr (linear in vy, r and delta,
+  // rational in vx) and of the rotation f0, f1 in psi.  tests/test_ode_cpu.py checks both
+  // against complex steps of f.
+  static constexpr int kVOff = 2;  // v[0..3] = x[kVOff..kVOff+3]
+  struct Cst {
+    double im, iJ, a, b, C;
+  };
+  __device__ __forceinline__ static Cst cst(const double* par) {
+    return {1.0 / par[0], 1.0 / par[4], par[1], par[2], 2.0 * par[3]};
+  }
+  struct Blk {  // one stage point: what f's Jacobian and the Hessian of mu^T f need
+    double vx, vy, r, sp, cp, w, P1, P2, Fyf, f0, f1;
+  };
+  __device__ __forceinline__ static Blk blk(const double* x, double d, double sp, double cp, double w, const Cst& k) {
+    Blk s;
+    s.vx = x[3];
+    s.vy = x[4];
+    s.r = x[5];
+    s.sp = sp;
+    s.cp = cp;
+    s.w = w;
+    s.P1 = fma(k.a, s.r, s.vy);
+    s.P2 = fma(-k.b, s.r, s.vy);
+    s.Fyf = k.C * fma(-s.P1, w, d);
+    s.f0 = s.vx * cp - s.vy * sp;
+    s.f1 = s.vx * sp + s.vy * cp;
+    return s;
+  }
+  struct MuQ {  // the parts of an adjoint mu that its Hessian term needs
+    double m0, m1, m3, m4, al, be, alp;  // alp = d al / d delta
+  };
+  __device__ __forceinline__ static MuQ muq(const double* mu, double sd, double cd, const Cst& k) {
+    const double gam = fma(mu[5] * k.a, k.iJ, mu[4] * k.im);
+    const double m3 = mu[3] * k.im;
+    return {mu[0], mu[1], mu[3], mu[4], fma(gam, cd, -m3 * sd), fma(-mu[5] * k.b, k.iJ, mu[4] * k.im), -fma(m3, cd, gam * sd)};
+  }
+  // g = (d f / d(psi, vx, vy, r))^T mu
+  __device__ __forceinline__ static void jt(const Blk& s, const double* mu, const MuQ& q, const Cst& k, double* g) {
+    const double w2 = s.w * s.w, Cw = k.C * s.w;
+    g[0] = fma(mu[1], s.f0, -mu[0] * s.f1);
+    g[1] = fma(mu[0], s.cp, fma(mu[1], s.sp, fma(-mu[4], s.r, k.C * w2 * fma(s.P1, q.al, s.P2 * q.be))));
+    g[2] = fma(mu[1], s.cp, fma(-mu[0], s.sp, fma(mu[3], s.r, -Cw * (q.al + q.be))));
+    g[3] = mu[2] + fma(mu[3], s.vy, fma(-mu[4], s.vx, -Cw * fma(k.a, q.al, -k.b * q.be)));
+  }
+  // d f / dv: the rows of f3, f4, f5 over (vx, vy, r, delta) (the other entries are
+  // -f1, cp, -sp / f0, sp, cp in rows 0, 1, the 1 of f2 in r and of f3 in ax)
+  struct Jac {
+    double j3[4], j4[4], j5[4];
+  };
+  __device__ __forceinline__ static Jac jac(const Blk& s, double sd, double cd, const Cst& k) {
+    const double w2 = s.w * s.w;
+    const double fvx = k.C * s.P1 * w2, fvy = -k.C * s.w, fr = -k.C * k.a * s.w;  // d Fyf
+    const double rvx = k.C * s.P2 * w2, rvy = -k.C * s.w, rr = k.C * k.b * s.w;   // d Fyr
+    const double sdm = sd * k.im;
+    Jac J;
+    J.j3[0] = -fvx * sdm;
+    J.j3[1] = fma(-fvy, sdm, s.r);
+    J.j3[2] = fma(-fr, sdm, s.vy);
+    J.j3[3] = -fma(k.C, sd, s.Fyf * cd) * k.im;
+    J.j4[0] = fma(fma(fvx, cd, rvx), k.im, -s.r);
+    J.j4[1] = fma(fvy, cd, rvy) * k.im;
+    J.j4[2] = fma(fma(fr, cd, rr), k.im, -s.vx);
+    J.j4[3] = fma(k.C, cd, -s.Fyf * sd) * k.im;
+    J.j5[0] = fma(k.a * fvx, cd, -k.b * rvx) * k.iJ;
+    J.j5[1] = fma(k.a * fvy, cd, -k.b * rvy) * k.iJ;
+    J.j5[2] = fma(k.a * fr, cd, -k.b * rr) * k.iJ;
+    J.j5[3] = k.a * fma(k.C, cd, -s.Fyf * sd) * k.iJ;
+    return J;
+  }
+  // the Hessian of mu^T f over v = (psi, vx, vy, r, delta) (ax enters linearly): its 11
+  // structural non-zeros pp, pvx, pvy, xx, xy, xr, xd, yr, yd, rd, dd (vy-vy, r-r, psi-r and
+  // psi-delta are zero)
+  struct Hes {
+    double pp, pvx, pvy, xx, xy, xr, xd, yr, yd, rd, dd;
+  };
+  __device__ __forceinline__ static Hes hes(const Blk& s, const MuQ& q, const Cst& k) {
+    const double w2 = s.w * s.w, Cw = k.C * s.w, Cw2 = k.C * w2;
+    Hes W;
+    W.pp = -fma(q.m0, s.f0, q.m1 * s.f1);
+    W.pvx = fma(-q.m0, s.sp, q.m1 * s.cp);
+    W.pvy = -fma(q.m0, s.cp, q.m1 * s.sp);
+    W.xx = -2.0 * Cw2 * s.w * fma(s.P1, q.al, s.P2 * q.be);
+    W.xy = Cw2 * (q.al + q.be);
+    W.xr = fma(Cw2, fma(k.a, q.al, -k.b * q.be), -q.m4);
+    W.xd = Cw2 * s.P1 * q.alp;
+    W.yr = q.m3;
+    W.yd = -Cw * q.alp;
+    W.rd = -Cw * k.a * q.alp;
+    W.dd = fma(2.0 * k.C, q.alp, -s.Fyf * q.al);
+    return W;
+  }
 };
 
 struct CartPole {
@@ -199,6 +344,7 @@ struct CartPole {
   static constexpr unsigned NLMASK = (1u << 1) | (1u << 2) | (1u << 3) | (1u << 4);  // p', phi, phi', F
   static constexpr unsigned INDEP = (1u << 0);                                        // f does not read p
   static constexpr int kTrigPerEval = 3, kTrigInput = 0, kTrigMaxM = 1;  // sincos(phi), 1/(M + m sin^2 phi)
+  static constexpr bool kAdjoint = false;
   template <class S, class Tc>
   __device__ __forceinline__ static void f(const S* x, const S* u, const double* par, S* dx, Tc& tc) {
     // par = (M, m, L, g, c); phi measured so that the upright linearisation is the reference's Ac
@@ -223,6 +369,7 @@ __device__ __forceinline__ void ode_rk4(const S* x0, const S* u, const OdeParams
   const double h = op.h;
 #pragma unroll 1
   for (int s = 0; s < op.M; ++s) {
+    tc.template substep<NX>(s, x);
     S acc[NX], xt[NX], k[NX];
 #pragma unroll
     for (int i = 0; i < NX; ++i) xt[i] = x[i];
@@ -326,8 +473,211 @@ struct OdeModel {
     }
     q = acc;
   }
+  // F, q and their exact derivatives at z for the adjoint ln: the adjoint path where the model
+  // has closed-form partials and its checkpoints fit this lane's LDS column, else hyper-dual passes
   __device__ __forceinline__ static void derivs(const ModelArgs& a, const Ctx& c, const double* z, const double* ln, double fs,
                                                 double* xf, double& q, double* A, double* Bm, double* g, double* H) {
+    if constexpr (Dyn::kAdjoint) {
+      if (a.tc != nullptr && 2 * NX * a.op.M <= kTrigSlots) {  // kernel-uniform
+        derivs_adjoint(a, c, z, ln, fs, xf, q, A, Bm, g, H);
+        return;
+      }
+    }
+    derivs_passes(a, c, z, ln, fs, xf, q, A, Bm, g, H);
+  }
+  // the mpctools node cost: q, its gradient and (diagonal) Hessian, scaled by fs
+  __device__ __forceinline__ static void cost_derivs(const ModelArgs& a, const Ctx& c, const double* z, double fs,
+                                                     double* g, double* H) {
+#pragma unroll
+    for (int i = 0; i < NH; ++i) H[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+      const double w2 = 2.0 * fs * wgt(a, i);
+      g[i] = w2 * (z[i] - c.zr[i]);
+      H[symix(i, i, NZ)] = w2;
+    }
+  }
+  // Exact derivatives by forward sensitivities and stage adjoints (Dyn::kAdjoint: closed-form
+  // partials of f).  Everything in RK4 but f is linear, so with mu_e the adjoint of stage e's f
+  // value in lam^T F and Tv_e = dv_e/dz the sensitivity of the variables f reads at stage e,
+  //   d2(lam^T F)/dz2 = sum_e Tv_e^T [d2(mu_e^T f)/dv2] Tv_e        (e over the 4 M stages).
+  // Three passes over the interval: (A) the value as value() computes it, storing the state at
+  // each substep start to this lane's LDS column; (B) backwards, the adjoint at each substep end
+  // (stored next to them); (C) forwards, per substep: its stage points again, the stage adjoints
+  // from the stored lam_{s+1}, then the sensitivities (6 x 6 over v) and the Hessian terms.
+  // The 6-state bicycle (M = 4): ~14 k FP64 flops per interval against 107 k for its 21
+  // hyper-dual passes (tests/test_gpu_ode.py compares the two).
+  __device__ static void derivs_adjoint(const ModelArgs& a, const Ctx& c, const double* z, const double* ln, double fs,
+                                        double* xf, double& q, double* A, double* Bm, double* g, double* H) {
+    using D = Dyn;
+    constexpr int NV = 6, VO = D::kVOff;  // v = (psi, vx, vy, r, delta, ax) = z[VO .. VO + 5]
+    static_assert(NX == 6 && NU == 2 && VO == 2, "adjoint path written for the 6-state bicycle");
+    using Blk = typename D::Blk;
+    using MuQ = typename D::MuQ;
+    const int M = a.op.M;
+    const double h = a.op.h;
+    double* ck = a.tc;  // slots [NX s, NX s + NX): x_s; [NX (M + s), ...): lam_{s+1}
+    const int cs = a.tc_stride;
+    const auto K = D::cst(a.op.par);
+    const double* u = z + NX;
+    double sd, cd;
+    ::sincos(u[0], &sd, &cd);
+    {  // (A)
+      TrigAdj ta{ck, cs, sd, cd, 0.0, 0.0, 0.0};
+      value_tc(a, c, z, xf, q, ta);
+    }
+    cost_derivs(a, c, z, fs, g, H);
+    // stage points of substep s, from its checkpoint
+    auto stages = [&](int s, Blk* B) __attribute__((always_inline)) {
+      double x[NX], xt[NX];
+#pragma unroll
+      for (int i = 0; i < NX; ++i) xt[i] = x[i] = ck[(NX * s + i) * cs];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        TrigAdj tc{nullptr, 0, sd, cd, 0.0, 0.0, 0.0};
+        double k[NX];
+        D::f(xt, u, a.op.par, k, tc);
+        B[e] = D::blk(xt, u[0], tc.sx, tc.cx, tc.rx, K);
+        if (e < 3) {
+          const double cn = (e == 2) ? h : 0.5 * h;
+#pragma unroll
+          for (int i = 0; i < NX; ++i) xt[i] = x[i] + cn * k[i];
+        }
+      }
+    };
+    // stage adjoints of a substep from l = lam_{s+1}; l becomes lam_s
+    auto reverse = [&](const Blk* B, double* l, MuQ* Q) __attribute__((always_inline)) {
+      double gn[4] = {0.0, 0.0, 0.0, 0.0}, gs[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int e = 3; e >= 0; --e) {
+        const double cl = (e == 0 || e == 3) ? h / 6.0 : h / 3.0;  // dx_{s+1}/dk_e
+        const double cg = (e == 2) ? h : 0.5 * h;                  // dxt_{e+1}/dk_e
+        double mu[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+          mu[i] = cl * l[i];
+          if (e < 3 && i >= VO && i < VO + 4) mu[i] = fma(cg, gn[i - VO], mu[i]);
+        }
+        Q[e] = D::muq(mu, sd, cd, K);
+        D::jt(B[e], mu, Q[e], K, gn);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gs[j] += gn[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) l[VO + j] += gs[j];
+    };
+    {  // (B)
+      double l[NX];
+#pragma unroll
+      for (int i = 0; i < NX; ++i) l[i] = ln[i];
+#pragma unroll 1
+      for (int s = M - 1; s >= 0; --s) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) ck[(NX * (M + s) + i) * cs] = l[i];
+        if (s == 0) break;
+        Blk B[4];
+        MuQ Q[4];
+        stages(s, B);
+        reverse(B, l, Q);
+      }
+    }
+    // (C)
+    double Tx[NX][NV], Hv[NV * (NV + 1) / 2];
+#pragma unroll
+    for (int r = 0; r < NX; ++r)
+#pragma unroll
+      for (int j = 0; j < NV; ++j) Tx[r][j] = (r >= VO && r - VO == j) ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 0; i < NV * (NV + 1) / 2; ++i) Hv[i] = 0.0;
+#pragma unroll 1
+    for (int s = 0; s < M; ++s) {
+      Blk B[4];
+      MuQ Q[4];
+      stages(s, B);
+      {
+        double l[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) l[i] = ck[(NX * (M + s) + i) * cs];
+        reverse(B, l, Q);
+      }
+      double acc[NX][NV], Tt[4][NV];  // Tt: the stage point's (psi, vx, vy, r) rows
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < NV; ++j) Tt[r][j] = Tx[VO + r][j];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto W = D::hes(B[e], Q[e], K);
+        // Hv += Tv^T W Tv, Tv = (Tt; e_delta; e_ax)
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          const double tp = Tt[0][j], tx = Tt[1][j], ty = Tt[2][j], tr = Tt[3][j];
+          double wp = fma(W.pp, tp, fma(W.pvx, tx, W.pvy * ty));
+          double wx = fma(W.pvx, tp, fma(W.xx, tx, fma(W.xy, ty, W.xr * tr)));
+          double wy = fma(W.pvy, tp, fma(W.xy, tx, W.yr * tr));
+          double wr = fma(W.xr, tx, W.yr * ty);
+          double wd = fma(W.xd, tx, fma(W.yd, ty, W.rd * tr));
+          if (j == 4) {  // the delta column of Tv is e_delta
+            wx += W.xd;
+            wy += W.yd;
+            wr += W.rd;
+            wd += W.dd;
+          }
+#pragma unroll
+          for (int i = 0; i <= j; ++i) {
+            double v = fma(Tt[0][i], wp, fma(Tt[1][i], wx, fma(Tt[2][i], wy, Tt[3][i] * wr)));
+            if (i == 4) v += wd;
+            Hv[symix(i, j, NV)] += v;
+          }
+        }
+        // sensitivities: Tk = (df/dv) Tv, then the RK4 combination and the next stage point
+        const auto J = D::jac(B[e], sd, cd, K);
+        const double wa = (e == 0 || e == 3) ? 1.0 : 2.0;
+        const double cn = (e == 2) ? h : 0.5 * h;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          const double tp = Tt[0][j], tx = Tt[1][j], ty = Tt[2][j], tr = Tt[3][j];
+          double tk[NX];
+          tk[0] = fma(-B[e].f1, tp, fma(B[e].cp, tx, -B[e].sp * ty));
+          tk[1] = fma(B[e].f0, tp, fma(B[e].sp, tx, B[e].cp * ty));
+          tk[2] = tr;
+          tk[3] = fma(J.j3[0], tx, fma(J.j3[1], ty, J.j3[2] * tr));
+          tk[4] = fma(J.j4[0], tx, fma(J.j4[1], ty, J.j4[2] * tr));
+          tk[5] = fma(J.j5[0], tx, fma(J.j5[1], ty, J.j5[2] * tr));
+          if (j == 4) {
+            tk[3] += J.j3[3];
+            tk[4] += J.j4[3];
+            tk[5] += J.j5[3];
+          }
+          if (j == 5) tk[3] += 1.0;  // f3 = ax + ...
+#pragma unroll
+          for (int r = 0; r < NX; ++r) acc[r][j] = (e == 0) ? tk[r] : fma(wa, tk[r], acc[r][j]);
+          if (e < 3)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Tt[r][j] = fma(cn, tk[VO + r], Tx[VO + r][j]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < NX; ++r)
+#pragma unroll
+        for (int j = 0; j < NV; ++j) Tx[r][j] = fma(h / 6.0, acc[r][j], Tx[r][j]);
+    }
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+#pragma unroll
+      for (int j = 0; j < NX; ++j) A[r * NX + j] = (j < VO) ? (r == j ? 1.0 : 0.0) : Tx[r][j - VO];
+#pragma unroll
+      for (int l = 0; l < NU; ++l) Bm[r * NU + l] = Tx[r][NX - VO + l];
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = i; j < NV; ++j) H[symix(VO + i, VO + j, NZ)] += Hv[symix(i, j, NV)];
+  }
+  // derivatives by hyper-dual RK4 passes (every model; the 6-state bicycle's reference path)
+  __device__ __forceinline__ static void derivs_passes(const ModelArgs& a, const Ctx& c, const double* z, const double* ln,
+                                                       double fs, double* xf, double& q, double* A, double* Bm, double* g,
+                                                       double* H) {
     const bool cached = a.tc != nullptr && a.op.M <= kTrigMaxM;  // kernel-uniform
     if (cached) {
       TrigRecord rec{a.tc, a.tc_stride, Dyn::kTrigInput};

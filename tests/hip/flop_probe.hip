@@ -14,7 +14,9 @@
 
 namespace mpcx {
 
-template <class Model>
+// PASSES: the ODE models' hyper-dual pass derivatives (OdeModel::derivs_passes) instead of the
+// path the kernel takes (tests/test_gpu_ode.py compares the 6-state bicycle's adjoint path to it)
+template <class Model, bool PASSES = false>
 __global__ void eval_probe_kernel(int n, ModelArgs ma, const double* Z, const double* L, const double* P, int pstride,
                                   double* out) {
   constexpr int NX = Model::NX, NU = Model::NU, NZ = NX + NU, NH = NZ * (NZ + 1) / 2;
@@ -32,7 +34,10 @@ __global__ void eval_probe_kernel(int n, ModelArgs ma, const double* Z, const do
   for (int j = 0; j < NZ; ++j) z[j] = Z[(size_t)i * NZ + j];
   for (int j = 0; j < NX; ++j) ln[j] = L[(size_t)i * NX + j];
   double xf[NX], q, A[NX * NX], Bm[NX * NU], g[NZ], H[NH];
-  Model::derivs(ma, c, z, ln, 1.0, xf, q, A, Bm, g, H);
+  if constexpr (PASSES)
+    Model::derivs_passes(ma, c, z, ln, 1.0, xf, q, A, Bm, g, H);
+  else
+    Model::derivs(ma, c, z, ln, 1.0, xf, q, A, Bm, g, H);
   double* o = out + (size_t)i * NO;
   int t = 0;
   for (int j = 0; j < NX; ++j) o[t++] = xf[j];
@@ -81,10 +86,11 @@ __global__ void riccati_probe_kernel(int n, const double* in, double* out) {
   for (int j = 0; j < NU; ++j) o[t++] = kf[j];
 }
 
-template <class Model>
+template <class Model, bool PASSES = false>
 int launch_eval(int n, const ModelArgs& ma, const double* Z, const double* L, const double* P, int pstride, double* out) {
   const size_t lds = Model::kTrigSlots > 0 ? (size_t)Model::kTrigSlots * 64 * sizeof(double) : 0;
-  hipLaunchKernelGGL(eval_probe_kernel<Model>, dim3((n + 63) / 64), dim3(64), lds, 0, n, ma, Z, L, P, pstride, out);
+  hipLaunchKernelGGL((eval_probe_kernel<Model, PASSES>), dim3((n + 63) / 64), dim3(64), lds, 0, n, ma, Z, L, P, pstride,
+                     out);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return -1000 - (int)e;
   const hipError_t s = hipDeviceSynchronize();
@@ -104,11 +110,8 @@ int launch_riccati(int n, const double* in, double* out) {
 // model: 1 unicycle (cost 0 quadrature / 1 node), 3 kinematic bicycle, 4 dynamic bicycle,
 // 5 cart-pole (include/mpcx.h model ids).  Z: n x NZ, L: n x NX, P: n x pstride (x0 then the
 // reference), all device pointers; returns 0 on success.
-extern "C" int eval_probe(int model, int n, double T, int M, int cost, const double* Q, const double* R,
-                          const double* par, const double* Z, const double* L, const double* P, int pstride,
-                          double* out) {
+static mpcx::ModelArgs probe_args(double T, int M, int cost, const double* Q, const double* R, const double* par) {
   using namespace mpcx;
-  if (n <= 0 || n % 64 || M < 1) return -3;
   ModelArgs ma{};
   ma.p_layout = 0;
   ma.N = 1;
@@ -125,11 +128,35 @@ extern "C" int eval_probe(int model, int n, double T, int M, int cost, const dou
     ma.op.R[j] = R[j];
     ma.op.par[j] = par[j];
   }
+  return ma;
+}
+
+extern "C" int eval_probe(int model, int n, double T, int M, int cost, const double* Q, const double* R,
+                          const double* par, const double* Z, const double* L, const double* P, int pstride,
+                          double* out) {
+  using namespace mpcx;
+  if (n <= 0 || n % 64 || M < 1) return -3;
+  const ModelArgs ma = probe_args(T, M, cost, Q, R, par);
   switch (model) {
     case 1: return launch_eval<UnicycleModel>(n, ma, Z, L, P, pstride, out);
     case 3: return launch_eval<OdeModel<KinBicycle>>(n, ma, Z, L, P, pstride, out);
     case 4: return launch_eval<OdeModel<DynBicycle>>(n, ma, Z, L, P, pstride, out);
     case 5: return launch_eval<OdeModel<CartPole>>(n, ma, Z, L, P, pstride, out);
+    default: return -4;
+  }
+}
+
+// the ODE models through their hyper-dual passes (same arguments as eval_probe)
+extern "C" int eval_probe_passes(int model, int n, double T, int M, int cost, const double* Q, const double* R,
+                                 const double* par, const double* Z, const double* L, const double* P, int pstride,
+                                 double* out) {
+  using namespace mpcx;
+  if (n <= 0 || n % 64 || M < 1) return -3;
+  const ModelArgs ma = probe_args(T, M, cost, Q, R, par);
+  switch (model) {
+    case 3: return launch_eval<OdeModel<KinBicycle>, true>(n, ma, Z, L, P, pstride, out);
+    case 4: return launch_eval<OdeModel<DynBicycle>, true>(n, ma, Z, L, P, pstride, out);
+    case 5: return launch_eval<OdeModel<CartPole>, true>(n, ma, Z, L, P, pstride, out);
     default: return -4;
   }
 }

@@ -199,3 +199,53 @@ def test_dyn_bicycle_hardest_instances_are_kkt_points(mpcx):
     for b in hard:
         kkt, gres = pr.kkt_residual(r["w"][b], r["lam_g"][b], r["lam_x"][b], P[b])
         assert kkt <= 1e-6 and gres <= 1e-9, (b, int(r["iters"][b]), kkt, gres)
+
+
+def test_dyn_bicycle_adjoint_derivatives_match_passes():
+    """The 6-state bicycle's stage derivatives as the solve kernel forms them (ode.h
+    OdeModel::derivs_adjoint: forward sensitivities and stage adjoints through RK4, closed-form
+    partials of f) against its 21 hyper-dual RK4 passes (derivs_passes), both through the device
+    harness tests/hip/flop_probe.hip on 4096 random points of the model's domain: F, q and the cost
+    gradient bit-identical (the same value pass), A, B and the Hessian of q + lam^T F equal to
+    1e-11 relative to each point's largest entry (both exact up to rounding)."""
+    import ctypes
+
+    import torch
+    from mpcx import ode
+
+    lib = ctypes.CDLL(os.path.join(ROOT, "tests", "hip", "libflop_probe.so"))
+    vp = ctypes.c_void_p
+    for fn in (lib.eval_probe, lib.eval_probe_passes):
+        fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp, vp,
+                       ctypes.c_int, vp]
+    ocp = ode.dynamic_bicycle_lane_change()
+    nx, nu, n = 6, 2, 4096
+    nz = nx + nu
+    rng = np.random.default_rng(7)
+    Z = np.stack([rng.uniform(-50, 50, n), rng.uniform(-5, 5, n), rng.uniform(-math.pi, math.pi, n),
+                  rng.uniform(2.5, 30.0, n), rng.uniform(-2, 2, n), rng.uniform(-1, 1, n),
+                  rng.uniform(-0.5, 0.5, n), rng.uniform(-5, 5, n)], axis=1)
+    P = np.concatenate([Z[:, :nx], Z[:, :nx] + rng.normal(0, 1, (n, nx))], axis=1)
+    L = rng.normal(size=(n, nx)) * 10.0 ** rng.uniform(-2, 2, (n, 1))
+    arr8 = lambda v: (ctypes.c_double * 8)(*(list(v) + [0.0] * (8 - len(v))))  # noqa: E731
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda()  # noqa: E731
+    d_z, d_l, d_p = dev(Z), dev(L), dev(P)
+    no = nx + 1 + nx * nx + nx * nu + nz + nz * (nz + 1) // 2
+    outs = []
+    for fn in (lib.eval_probe, lib.eval_probe_passes):
+        out = torch.zeros(n * no, dtype=torch.float64, device="cuda")
+        rc = fn(4, n, ocp.T, ocp.M, 0, arr8(ocp.Q), arr8(ocp.R), arr8(ocp.par), vp(d_z.data_ptr()), vp(d_l.data_ptr()),
+                vp(d_p.data_ptr()), 2 * nx, vp(out.data_ptr()))
+        assert rc == 0
+        outs.append(out.cpu().numpy().reshape(n, no))
+    adj, ref = outs
+    assert np.isfinite(adj).all()
+    o_a = nx + 1
+    o_g = o_a + nx * nx + nx * nu
+    o_h = o_g + nz
+    np.testing.assert_array_equal(adj[:, :o_a], ref[:, :o_a])  # F, q
+    np.testing.assert_array_equal(adj[:, o_g:o_h], ref[:, o_g:o_h])  # cost gradient
+    for lo, hi, name in ((o_a, o_g, "A, B"), (o_h, no, "H")):
+        err = np.abs(adj[:, lo:hi] - ref[:, lo:hi]).max(axis=1) / np.maximum(np.abs(ref[:, lo:hi]).max(axis=1), 1e-300)
+        print(f"{name}: max relative difference {err.max():.2e}")
+        assert err.max() <= 1e-11, name
