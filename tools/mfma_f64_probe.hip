@@ -1,0 +1,127 @@
+// mfma_f64_probe.hip -- lane layouts and dependent-chain latencies of the FP64 MFMA instructions on
+// gfx950 (the Riccati chain design question: can a 4x4x4 / 16x16x4 f64 MFMA replace the one-lane
+// step?).  Build: hipcc --offload-arch=gfx950 -O3 tools/mfma_f64_probe.hip -o tools/mfma_f64_probe
+// Prints JSON: for each instruction, which (A lane, B lane) pairs feed each D element, and the
+// cycles (s_memtime) per MFMA of a dependent chain D -> C and D -> B.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// D lane/reg contents when A = one-hot at lane ta (value 1), B = one-hot at lane tb (value 1), C = 0
+__global__ void probe4(int ta, int tb, double* out) {
+  const int l = threadIdx.x;
+  const double a = l == ta ? 1.0 : 0.0, b = l == tb ? 1.0 : 0.0;
+  out[l] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, 0.0, 0, 0, 0);
+}
+__global__ void probe16(int ta, int tb, double* out) {
+  const int l = threadIdx.x;
+  const double a = l == ta ? 1.0 : 0.0, b = l == tb ? 1.0 : 0.0;
+  d4 c = {0.0, 0.0, 0.0, 0.0};
+  d4 d = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  for (int r = 0; r < 4; ++r) out[r * 64 + l] = d[r];
+}
+
+// dependent chains: kind 0 = D feeds C (accumulate), kind 1 = D feeds the B operand
+template <int KIND>
+__global__ void lat4(double* out, long long* cyc, int n) {
+  const int l = threadIdx.x;
+  double a = 1e-3 * (l + 1), b = 1.0 + 1e-4 * l, c = 0.0;
+  const long long t0 = __builtin_readcyclecounter();
+  for (int i = 0; i < n; ++i) {
+    const double d = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+    if (KIND == 0) c = d;
+    else b = d * 0.5;
+  }
+  const long long t1 = __builtin_readcyclecounter();
+  out[l] = c + b;
+  if (l == 0) *cyc = t1 - t0;
+}
+template <int KIND>
+__global__ void lat16(double* out, long long* cyc, int n) {
+  const int l = threadIdx.x;
+  double a = 1e-3 * (l + 1), b = 1.0 + 1e-4 * l;
+  d4 c = {0.0, 0.0, 0.0, 0.0};
+  const long long t0 = __builtin_readcyclecounter();
+  for (int i = 0; i < n; ++i) {
+    const d4 d = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    if (KIND == 0) c = d;
+    else b = d[0] * 0.5;
+  }
+  const long long t1 = __builtin_readcyclecounter();
+  out[l] = c[0] + c[1] + c[2] + c[3] + b;
+  if (l == 0) *cyc = t1 - t0;
+}
+// reference: a dependent chain of v_fma_f64 (one wave)
+__global__ void latfma(double* out, long long* cyc, int n) {
+  const int l = threadIdx.x;
+  double a = 1.0 + 1e-9 * l, c = 0.0;
+  const long long t0 = __builtin_readcyclecounter();
+  for (int i = 0; i < n; ++i) c = fma(a, c, 1e-3);
+  const long long t1 = __builtin_readcyclecounter();
+  out[l] = c;
+  if (l == 0) *cyc = t1 - t0;
+}
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));              \
+      return 1;                                                            \
+    }                                                                      \
+  } while (0)
+
+int main() {
+  double* d;
+  long long* cyc;
+  CK(hipMalloc(&d, 256 * sizeof(double)));
+  CK(hipMalloc(&cyc, sizeof(long long)));
+  std::vector<double> h(256);
+  printf("{\n \"mfma_f64_4x4x4_4b\": [");
+  // A lane ta and B lane tb contribute to D element (lane) iff out[lane] == 1
+  bool first = true;
+  for (int ta = 0; ta < 64; ++ta)
+    for (int tb = 0; tb < 64; ++tb) {
+      probe4<<<1, 64>>>(ta, tb, d);
+      CK(hipMemcpy(h.data(), d, 64 * sizeof(double), hipMemcpyDeviceToHost));
+      for (int l = 0; l < 64; ++l)
+        if (h[l] != 0.0) {
+          printf("%s[%d,%d,%d]", first ? "" : ",", ta, tb, l);
+          first = false;
+        }
+    }
+  printf("],\n \"mfma_f64_16x16x4\": [");
+  first = true;
+  for (int ta = 0; ta < 64; ++ta)
+    for (int tb = 0; tb < 64; ++tb) {
+      probe16<<<1, 64>>>(ta, tb, d);
+      CK(hipMemcpy(h.data(), d, 256 * sizeof(double), hipMemcpyDeviceToHost));
+      for (int r = 0; r < 4; ++r)
+        for (int l = 0; l < 64; ++l)
+          if (h[r * 64 + l] != 0.0) {
+            printf("%s[%d,%d,%d,%d]", first ? "" : ",", ta, tb, l, r);
+            first = false;
+          }
+    }
+  printf("],\n");
+  const int n = 4096;
+  long long c;
+  auto run = [&](void (*k)(double*, long long*, int), const char* name, bool last) -> int {
+    k<<<1, 64>>>(d, cyc, n);
+    CK(hipDeviceSynchronize());
+    k<<<1, 64>>>(d, cyc, n);
+    CK(hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost));
+    printf(" \"%s_cycles_per_op\": %.2f%s\n", name, (double)c / n, last ? "" : ",");
+    return 0;
+  };
+  if (run(lat4<0>, "lat4_d_to_c", false)) return 1;
+  if (run(lat4<1>, "lat4_d_to_b", false)) return 1;
+  if (run(lat16<0>, "lat16_d_to_c", false)) return 1;
+  if (run(lat16<1>, "lat16_d_to_b", false)) return 1;
+  if (run(latfma, "fma_f64_dep", true)) return 1;
+  printf("}\n");
+  return 0;
+}
