@@ -5,6 +5,8 @@
 // cycles (s_memtime) per MFMA of a dependent chain D -> C and D -> B.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <vector>
 
@@ -65,6 +67,19 @@ __global__ void latfma(double* out, long long* cyc, int n) {
   if (l == 0) *cyc = t1 - t0;
 }
 
+// v_rcp_f64 and its Newton refinements: out[3 i + m] = m Newton steps from v_rcp_f64 of x[i]
+__global__ void rcp_probe(const double* x, double* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double v = x[i];
+  double r = __builtin_amdgcn_rcp(v);
+  out[3 * i] = r;
+  r = fma(r, fma(-v, r, 1.0), r);
+  out[3 * i + 1] = r;
+  r = fma(r, fma(-v, r, 1.0), r);
+  out[3 * i + 2] = r;
+}
+
 #define CK(x)                                                              \
   do {                                                                     \
     hipError_t e_ = (x);                                                   \
@@ -121,7 +136,30 @@ int main() {
   if (run(lat4<1>, "lat4_d_to_b", false)) return 1;
   if (run(lat16<0>, "lat16_d_to_c", false)) return 1;
   if (run(lat16<1>, "lat16_d_to_b", false)) return 1;
-  if (run(latfma, "fma_f64_dep", true)) return 1;
+  if (run(latfma, "fma_f64_dep", false)) return 1;
+  // relative error of v_rcp_f64 with 0 / 1 / 2 Newton steps over 2^20 inputs spread over 1e-12..1e12
+  {
+    const int m = 1 << 20;
+    std::vector<double> hx(m), hr(3 * m);
+    unsigned long long st = 88172645463325252ull;
+    for (int i = 0; i < m; ++i) {
+      st ^= st << 13;
+      st ^= st >> 7;
+      st ^= st << 17;
+      const double u = (double)(st >> 11) / 9007199254740992.0;
+      hx[i] = std::pow(10.0, -12.0 + 24.0 * u) * ((st & 1) ? 1.0 : -1.0);
+    }
+    double *dx, *dr;
+    CK(hipMalloc(&dx, m * sizeof(double)));
+    CK(hipMalloc(&dr, 3 * m * sizeof(double)));
+    CK(hipMemcpy(dx, hx.data(), m * sizeof(double), hipMemcpyHostToDevice));
+    rcp_probe<<<m / 256, 256>>>(dx, dr, m);
+    CK(hipMemcpy(hr.data(), dr, 3 * m * sizeof(double), hipMemcpyDeviceToHost));
+    double e[3] = {0, 0, 0};
+    for (int i = 0; i < m; ++i)
+      for (int k = 0; k < 3; ++k) e[k] = std::max(e[k], std::fabs(hr[3 * i + k] * hx[i] - 1.0));
+    printf(" \"rcp_f64_max_rel_err\": [%.3e, %.3e, %.3e]\n", e[0], e[1], e[2]);
+  }
   printf("}\n");
   return 0;
 }
