@@ -255,13 +255,6 @@ __device__ __forceinline__ void group_next(const double* v, double* out, XWave<G
   }
 }
 
-// 1/x with ONE Newton step after v_rcp_f64 (max relative error 2.1e-15 against 4.6e-8 for
-// v_rcp_f64 alone and 1.1e-16 after two steps: profiles/r04_mfma_probe.json): two dependent FMAs
-// fewer than rcp64 where the reciprocal sits on a sequential chain
-__device__ __forceinline__ double rcp64_1(double x) {
-  const double r = __builtin_amdgcn_rcp(x);
-  return fma(r, fma(-x, r, 1.0), r);
-}
 // 1/x to full fp64 accuracy: v_rcp_f64 + two Newton steps (no IEEE division sequence
 // on the sequential critical path)
 __device__ __forceinline__ double rcp64(double x) {

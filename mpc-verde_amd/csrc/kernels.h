@@ -27,7 +27,6 @@
 #include <type_traits>
 
 #include "collectives.h"
-#include "mfma_chain.h"
 #include "models.h"
 #include "ode.h"
 #include "pscan.h"
@@ -247,17 +246,6 @@ struct ReplicateOf<M, std::void_t<decltype(M::kReplicate)>> {
   static constexpr bool value = M::kReplicate;
 };
 
-// Model::kMfmaChain if the model declares it: the sequential Riccati chain of a wave that holds
-// ONE instance runs on the matrix cores (mfma_chain.h); other group shapes keep the VALU chain
-template <class M, class = void>
-struct MfmaChainOf {
-  static constexpr bool value = false;
-};
-template <class M>
-struct MfmaChainOf<M, std::void_t<decltype(M::kMfmaChain)>> {
-  static constexpr bool value = M::kMfmaChain;
-};
-
 // R = 2 (replicated groups, G = 32): a batch too small to give every SIMD a wave runs one
 // instance per wave with its lane group held TWICE, in the wave's two 32-lane halves (replica rho
 // = lane / 32).  Both replicas compute the same bits (every collective is a 32-lane group
@@ -286,10 +274,6 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   // the matrix powers (A^T)^(j 4^l), j = 1..3, l < 5, kept for the launch (table index pow_tab)
   __shared__ double dscan[DecSuffixOf<Model>::value && G > 64 ? 2 * NX * kSBS + 15 * NX * NX : 1];
   double pow_tab = -1.0;  // table whose powers dscan holds (block-uniform)
-  // the MFMA Riccati chain (one instance per wave): per-node input and output records in LDS
-  constexpr bool kMfma = MfmaChainOf<Model>::value && ((G == 64 && R == 1) || (G == 32 && R == 2));
-  static_assert(!kMfma || (Model::NX == 3 && Model::NU == 2), "mfma_chain.h is written for NX = 3, NU = 2");
-  __shared__ double mcbuf[kMfma ? kMcLdsDoubles : 1];
   // workspace chain stash (solver.h chain_ws_slots): slots after the restoration workspace's
   constexpr bool kWsStash = WsStashOf<Model>::value;
   // The stash is one contiguous record per thread (array of structures, after the restoration
@@ -1315,16 +1299,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
           }
         }
         STAMP_SUB(12);
-        if constexpr (kMfma) {  // the chain on the matrix cores (mfma_chain.h; the launch keeps N <= kMcMaxN)
-          double* rin = mcbuf;
-          double* rout = mcbuf + (kMcMaxN + 1) * kMcIn;
-          if (hasX && rho == 0) mc_write_record(rin + k * kMcIn, Hd, gp, Aop, Bop, cdef, k == 0);
-          okl = mfma_chain(rin, rout, N);
-          if (hasU) {
-            mc_read_value(rout, k, P, p);
-            mc_read_gains(rout, k, Kk, kfk);
-          }
-        } else if constexpr (G <= 64) {
+        if constexpr (G <= 64) {
           if constexpr (kDec) {
             for (int j = N - 1; j >= jc; --j) {
               double pin_[NX];
@@ -1513,7 +1488,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
         }
       }
     }
-    if constexpr (!kMfma) riccati_gains<NX, NU>(fac, Kk, kfk);  // all lanes at once (the MFMA chain read them)
+    riccati_gains<NX, NU>(fac, Kk, kfk);  // all lanes at once
     if (k == 0)  // Hux'_0 = 0 (A_0 = 0): no feedback on X_0
 #pragma unroll
       for (int i = 0; i < NU * NX; ++i) Kk[i] = 0.0;

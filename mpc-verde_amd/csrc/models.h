@@ -41,8 +41,6 @@ struct UnicycleModel {
   // a 32-lane group widened to a whole wave runs as two replicas that split the sequential work
   // (kernels.h R = 2): configs 1-2 (N <= 30) at batches below two waves per SIMD
   static constexpr bool kReplicate = true;
-  // the Riccati chain of a one-instance wave on the matrix cores (mfma_chain.h)
-  static constexpr bool kMfmaChain = true;
   struct Ctx {
     double xr[3], ur[2];
   };
@@ -95,7 +93,6 @@ struct UnicycleFreeModel : UnicycleModel {
 struct UnicycleScanModel : UnicycleModel {
   static constexpr bool kParallelRiccati = true;
   static constexpr bool kReplicate = false;  // no sequential chain to split
-  static constexpr bool kMfmaChain = false;  // (its sequential fallback keeps the VALU chain)
 };
 
 // ------------------------------------------------------------------------------------

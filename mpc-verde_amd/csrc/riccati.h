@@ -260,11 +260,7 @@ __device__ __forceinline__ bool riccati_step(const double* Hd, const double* gp,
     const double a = Huu[0], b = Huu[1], d = Huu[3];
     const double det = fma(a, d, -b * b);
     ok = (a > 0.0) && (det > 0.0);
-#if defined(MPCX_RIC_NR) && MPCX_RIC_NR == 1
-    const double ra = rcp64_1(a), rdet = rcp64_1(det);  // experiment: one Newton step
-#else
     const double ra = rcp64(a), rdet = rcp64(det);  // independent
-#endif
     f.r0 = ra;
     f.t = b * ra;
     f.r1 = a * rdet;  // 1 / (d - b^2/a)

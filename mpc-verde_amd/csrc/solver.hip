@@ -10,7 +10,6 @@
 #include <cstdint>
 #include <cstdlib>
 
-#include "mfma_chain.h"
 #include "solver.h"
 #include "unicycle.h"
 
@@ -120,9 +119,7 @@ MPCX_DECLARE(cartpole)
 // UnicycleScanModel): ceil(log2(N+1)) = 5 combine levels cost about as much as 25 chain steps
 constexpr int kUnicycleScanMinN = 25;
 // diagnostic knob: MPCX_UNICYCLE_SCAN_MIN_N overrides it (A/B of the two instantiations).  Only
-// a whole number in [1, 256] is taken; anything else keeps the default.  Horizons beyond the MFMA
-// chain's records (kMcMaxN) take the scan whatever the knob says: the chain instantiations are
-// built for N <= kMcMaxN only (kernels.h kMfma).
+// a whole number in [1, 256] is taken (256: the scan never runs); anything else keeps the default.
 static int unicycle_scan_min_n() {
   static const int n = [] {
     const char* e = getenv("MPCX_UNICYCLE_SCAN_MIN_N");
@@ -139,7 +136,7 @@ static int unicycle_scan_min_n() {
 #define MPCX_DISPATCH(a, FN, ...)                                                 \
   do {                                                                            \
     if ((a).model == 1)                                                           \
-      return ((a).N >= unicycle_scan_min_n() || (a).N > kMcMaxN) ? FN##_unicycle_scan(__VA_ARGS__)      \
+      return (a).N >= unicycle_scan_min_n() ? FN##_unicycle_scan(__VA_ARGS__)                              \
              : (a).xbnd ? FN##_unicycle(__VA_ARGS__) : FN##_unicycle_xfree(__VA_ARGS__);                       \
     if ((a).model == 2 && (a).nx == 4 && (a).nu == 1) return FN##_linear4(__VA_ARGS__); \
     if ((a).model == 2 && (a).nx == 5 && (a).nu == 1) return FN##_linear5(__VA_ARGS__); \

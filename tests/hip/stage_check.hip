@@ -3,7 +3,6 @@
 // weighted-moment assembly the solve kernel uses) and uni_derivs<true> (the per-point formula)
 // at the same (x, u, x_ref, u_ref, lam, fs).  Built into tests/hip/libstage_check.so; used by
 // tests/test_gpu_stage.py only.
-#include "mfma_chain.h"
 #include "models.h"
 #include "riccati.h"
 #include "unicycle.h"
@@ -74,32 +73,6 @@ __global__ void riccati_check_kernel(int n, const double* in, double* out) {
   for (int j = 0; j < 2; ++j) o[16 + j] = kf[j];
 }
 
-// the MFMA Riccati chain (mfma_chain.h) of one wave per problem: N + 1 node records in, per
-// node k < N: P_k 6 (packed), p_k 3, K_k 6, kf_k 2 out, then the inertia verdict (17 N + 1
-// doubles per problem).  in per node: Hd 15, gp 5, A 9, B 6, c 3 (38 doubles); node N's Hd / gp
-// carry the terminal value function (x blocks).
-__global__ __launch_bounds__(64) void mfma_chain_check_kernel(int N, const double* in, double* out) {
-  __shared__ double buf[kMcLdsDoubles];
-  const int k = threadIdx.x;
-  const double* v = in + ((size_t)blockIdx.x * (N + 1) + (k <= N ? k : 0)) * 38;
-  double* rin = buf;
-  double* rout = buf + (kMcMaxN + 1) * kMcIn;
-  if (k <= N) mc_write_record(rin + k * kMcIn, v, v + 15, v + 20, v + 29, v + 35, false);
-  const bool ok = mfma_chain(rin, rout, N);
-  double* o = out + (size_t)blockIdx.x * (17 * N + 1);
-  if (k < N) {
-    double P[6], p[3], K[6], kf[2];
-    mc_read_value(rout, k, P, p);
-    mc_read_gains(rout, k, K, kf);
-    double* ok_ = o + 17 * k;
-    for (int j = 0; j < 6; ++j) ok_[j] = P[j];
-    for (int j = 0; j < 3; ++j) ok_[6 + j] = p[j];
-    for (int j = 0; j < 6; ++j) ok_[9 + j] = K[j];
-    for (int j = 0; j < 2; ++j) ok_[15 + j] = kf[j];
-  }
-  if (k == 0) o[17 * N] = ok ? 1.0 : 0.0;
-}
-
 }  // namespace mpcx
 
 extern "C" int riccati_check(int n, const double* in, double* out) {
@@ -135,13 +108,4 @@ extern "C" int stage_check(int n, double T, int M, int cost, const double* Q, co
                            const double* U, const double* XR, const double* UR, const double* L, double fs,
                            double* out) {
   return stage_check_which(n, T, M, cost, Q, R, X, U, XR, UR, L, fs, out, 0);
-}
-
-extern "C" int mfma_chain_check(int n, int N, const double* in, double* out) {
-  if (n <= 0 || N < 1 || N > mpcx::kMcMaxN) return -3;
-  hipLaunchKernelGGL(mpcx::mfma_chain_check_kernel, dim3(n), dim3(64), 0, 0, N, in, out);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return -1000 - (int)e;
-  const hipError_t s = hipDeviceSynchronize();
-  return s == hipSuccess ? 0 : -2000 - (int)s;
 }

@@ -312,9 +312,7 @@ def test_group_policy_same_results(mpcx, N, B):
     the same results.  Widening a 16-lane group (N = 10) or running one multi-wave group adds exact
     zeros / neutral values to every reduction: the same bits.  A 32-lane group widened to a wave
     (N = 20) runs replicated (kernels.h R = 2), and its replicas split the stage evaluation's RK4
-    substeps, summing the quadrature moments in two halves; and a wave that holds one instance
-    (N = 10 widened, N = 20 replicated) runs its Riccati chain on the matrix cores (mfma_chain.h),
-    which sums the step's products in the MFMA's order: there the same statuses and iteration
+    substeps, summing the quadrature moments in two halves: there the same statuses and iteration
     counts and a solution within 1e-9 (relative) of the narrow group's.  Policy 1 is also how the
     narrow-group code paths stay covered at test batch sizes."""
     ocp = mpcx.unicycle_point_to_point(N=N)
@@ -322,9 +320,9 @@ def test_group_policy_same_results(mpcx, N, B):
     r0 = mpcx.nlpsol("s", "mi355x", ocp).solve_batch(P)
     r1 = mpcx.nlpsol("s", "mi355x", ocp, {"group_policy": 1}).solve_batch(P)
     assert np.all(r0["status"] == 0)
-    one_per_wave = N < 32  # replicated (N >= 16) or widened, and the MFMA chain (kernels.h kMfma)
+    replicated = 16 <= N < 32
     for n in ("w", "f", "lam_g", "lam_x", "status", "iters"):
-        if one_per_wave and n in ("w", "f", "lam_g", "lam_x"):
+        if replicated and n in ("w", "f", "lam_g", "lam_x"):
             scale = np.maximum(np.max(np.abs(r1[n]), axis=-1, keepdims=True) if r1[n].ndim > 1 else np.abs(r1[n]), 1.0)
             assert np.max(np.abs(r0[n] - r1[n]) / scale) <= 1e-9, n
         else:

@@ -150,53 +150,3 @@ def test_riccati_step_vs_dense_formula(harness):
         cond = np.linalg.cond(Huu[pd])[:, None]
         err = np.abs(got - ref) / scale / np.maximum(cond, 1.0)
         assert err.max() <= 1e-12, err.max()
-
-
-def test_mfma_chain_vs_dense_recursion(harness):
-    """The Riccati chain on the matrix cores (csrc/mfma_chain.h: 4x4x4 FP64 MFMAs on the augmented
-    state (x, 1), one wave per chain) against the dense sequential recursion in numpy, N = 20 and
-    the LDS bound 31: P_k, p_k, K_k, kf_k of every node (<= 1e-10 relative to each problem's scale
-    and the conditioning of its Huu') and the inertia verdict (every step's Huu' positive
-    definite) on chains where some step is indefinite."""
-    import torch
-
-    harness.mfma_chain_check.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
-    rng = np.random.default_rng(11)
-    T = 0.2
-    for N, n in ((20, 256), (31, 64), (1, 16)):
-        A = np.tile(np.eye(3), (n, N + 1, 1, 1))
-        A[..., 0, 2], A[..., 1, 2] = rng.normal(size=(n, N + 1)) * 0.3, rng.normal(size=(n, N + 1)) * 0.3
-        Bm = np.zeros((n, N + 1, 3, 2))
-        Bm[..., 0:2, :] = rng.normal(size=(n, N + 1, 2, 2)) * 0.2
-        Bm[..., 2, 1] = T
-        L = rng.normal(size=(n, N + 1, 5, 5))
-        Hd = np.einsum("bnij,bnkj->bnik", L, L) * 0.2 + 0.1 * np.eye(5)
-        Hd[n // 2:, N // 2, 3:, 3:] -= 3.0 * np.eye(2)  # half of the problems: one indefinite stage
-        gp, c = rng.normal(size=(n, N + 1, 5)), rng.normal(size=(n, N + 1, 3)) * 0.1
-        inp = np.concatenate([pack(Hd), gp, A.reshape(n, N + 1, 9), Bm.reshape(n, N + 1, 6), c], axis=2)
-        d_in = torch.from_numpy(np.ascontiguousarray(inp)).cuda()
-        d_out = torch.zeros(n * (17 * N + 1), dtype=torch.float64, device="cuda")
-        assert harness.mfma_chain_check(n, N, ctypes.c_void_p(d_in.data_ptr()), ctypes.c_void_p(d_out.data_ptr())) == 0
-        o = d_out.cpu().numpy().reshape(n, 17 * N + 1)
-        for b in range(n):
-            P, p = Hd[b, N, :3, :3], gp[b, N, :3]
-            okref = True
-            for k in range(N - 1, -1, -1):
-                M = np.concatenate([A[b, k], Bm[b, k]], axis=1)
-                H = Hd[b, k] + M.T @ P @ M
-                g = gp[b, k] + M.T @ (P @ c[b, k] + p)
-                Huu, Hux, gu = H[3:, 3:], H[3:, :3], g[3:]
-                okref = okref and bool(np.all(np.linalg.eigvalsh(Huu) > 0))
-                K = -np.linalg.solve(Huu, Hux)
-                kf = -np.linalg.solve(Huu, gu)
-                P = H[:3, :3] + Hux.T @ K
-                P = 0.5 * (P + P.T)
-                p = g[:3] + Hux.T @ kf
-                if okref:  # values past an indefinite step are not compared
-                    got = o[b, 17 * k:17 * k + 17]
-                    scale = max(np.max(np.abs(P)), np.max(np.abs(K)), 1.0) * max(np.linalg.cond(Huu), 1.0)
-                    for gv, rv in ((got[0:6], pack(P)), (got[6:9], p), (got[9:15], K.reshape(6)), (got[15:17], kf)):
-                        err = np.max(np.abs(gv - rv)) / scale
-                        assert err <= 1e-10, (N, b, k, err)
-            assert (o[b, 17 * N] == 1.0) == okref, (N, b)
-        assert 0 < sum(o[b, 17 * N] == 1.0 for b in range(n)) < n or N == 1

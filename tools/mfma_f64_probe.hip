@@ -32,10 +32,13 @@ __global__ void lat4(double* out, long long* cyc, int n) {
   const int l = threadIdx.x;
   double a = 1e-3 * (l + 1), b = 1.0 + 1e-4 * l, c = 0.0;
   const long long t0 = __builtin_readcyclecounter();
-  for (int i = 0; i < n; ++i) {
-    const double d = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
-    if (KIND == 0) c = d;
-    else b = d * 0.5;
+  for (int i = 0; i < n; i += 16) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {  // unrolled: no loop branch between the dependent operations
+      const double d = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+      if (KIND == 0) c = d;
+      else b = d;
+    }
   }
   const long long t1 = __builtin_readcyclecounter();
   out[l] = c + b;
@@ -47,21 +50,44 @@ __global__ void lat16(double* out, long long* cyc, int n) {
   double a = 1e-3 * (l + 1), b = 1.0 + 1e-4 * l;
   d4 c = {0.0, 0.0, 0.0, 0.0};
   const long long t0 = __builtin_readcyclecounter();
-  for (int i = 0; i < n; ++i) {
-    const d4 d = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-    if (KIND == 0) c = d;
-    else b = d[0] * 0.5;
+  for (int i = 0; i < n; i += 16) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const d4 d = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+      if (KIND == 0) c = d;
+      else b = d[0];
+    }
   }
   const long long t1 = __builtin_readcyclecounter();
   out[l] = c[0] + c[1] + c[2] + c[3] + b;
   if (l == 0) *cyc = t1 - t0;
 }
-// reference: a dependent chain of v_fma_f64 (one wave)
+// reference: a dependent chain of v_fma_f64 (one wave), and of independent ones (issue rate)
+__global__ void indfma(double* out, long long* cyc, int n) {
+  const int l = threadIdx.x;
+  double a = 1.0 + 1e-9 * l, c[8];
+  for (int j = 0; j < 8; ++j) c[j] = 1e-3 * j;
+  const long long t0 = __builtin_readcyclecounter();
+  for (int i = 0; i < n; i += 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = fma(a, c[j], 1e-3);  // 8 independent chains: 4 ops per i
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = fma(a, c[j], 1e-3);
+  }
+  const long long t1 = __builtin_readcyclecounter();
+  double t = 0;
+  for (int j = 0; j < 8; ++j) t += c[j];
+  out[l] = t;
+  if (l == 0) *cyc = (t1 - t0) / 8;  // cycles per n of these = per 8 instructions / 8
+}
 __global__ void latfma(double* out, long long* cyc, int n) {
   const int l = threadIdx.x;
   double a = 1.0 + 1e-9 * l, c = 0.0;
   const long long t0 = __builtin_readcyclecounter();
-  for (int i = 0; i < n; ++i) c = fma(a, c, 1e-3);
+  for (int i = 0; i < n; i += 16) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) c = fma(a, c, 1e-3);
+  }
   const long long t1 = __builtin_readcyclecounter();
   out[l] = c;
   if (l == 0) *cyc = t1 - t0;
@@ -137,6 +163,7 @@ int main() {
   if (run(lat16<0>, "lat16_d_to_c", false)) return 1;
   if (run(lat16<1>, "lat16_d_to_b", false)) return 1;
   if (run(latfma, "fma_f64_dep", false)) return 1;
+  if (run(indfma, "fma_f64_indep_issue", false)) return 1;
   // relative error of v_rcp_f64 with 0 / 1 / 2 Newton steps over 2^20 inputs spread over 1e-12..1e12
   {
     const int m = 1 << 20;
