@@ -507,6 +507,11 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   };
   // fresh: xf .. c0 hold the evaluation at the current (z, lam) (group-uniform)
   bool fresh = false;
+  // lz_ok: Lz holds this lane's barrier log-sum at the current z -- the line search's first trial
+  // point, accepted as it stands (the update's z is that trial's zt bit for bit), so the next
+  // iteration's barrier objective needs no second evaluation of the same logarithms
+  bool lz_ok = false;
+  double Lz = 0.0;
   auto sweep = [&]() __attribute__((always_inline)) {
     eval_at(z, lam);
     fresh = true;
@@ -629,6 +634,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
       }
       init_point();
       fresh = false;
+      lz_ok = false;
       mu = warm ? a.mu_init : 0.1;
       tau = fmax(kTauMin, 1.0 - mu);
       fs = 1.0;
@@ -1700,7 +1706,8 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     STAMP(6);
     phase();
     // ------------------------------------------------------------ filter line search
-    double thk_l = 0, phk_l = (hasU ? fs * qv : 0.0) - mu * barrier_logsum<NZ>(z, lb, ub, hL, hU);
+    double thk_l = 0, phk_l = (hasU ? fs * qv : 0.0) - mu * (lz_ok ? Lz : barrier_logsum<NZ>(z, lb, ub, hL, hU));
+    lz_ok = false;
 #pragma unroll
     for (int i = 0; i < NX; ++i) thk_l += fabs(cdef[i]) + fabs(c0[i]);
     double tp[2] = {thk_l, phk_l};
@@ -1717,10 +1724,22 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     soft_tried = false;
     // switching condition alpha (-gd)^s_phi > delta theta^s_theta  <=>  alpha > sw_a with
     // sw_a = delta theta^s_theta / (-gd)^s_phi -- also the third term of alpha_min; one exp of
-    // logs, loop-invariant over the trials
-    const double sw_a = gd < 0 ? exp(log(kDeltaSw) + kSTheta * log(thk) - kSPhi * log(-gd)) : 0.0;
-    const double amin = gd < 0 ? kGammaAlpha * fmin(kGammaTheta, fmin(kGammaPhi * thk / (-gd), sw_a))
-                               : kGammaAlpha * kGammaTheta;
+    // logs, loop-invariant over the trials.  A long dependent chain of scalar operations: the
+    // models whose first trial evaluates derivatives form it beside that evaluation (same basic
+    // block, so the scheduler interleaves the two), the others here
+    double sw_a = 0.0, amin = kGammaAlpha * kGammaTheta;
+    bool sw_set = false;
+    auto switching = [&]() __attribute__((always_inline)) {
+      if (gd < 0) {
+        sw_a = exp(log(kDeltaSw) + kSTheta * log(thk) - kSPhi * log(-gd));
+        amin = kGammaAlpha * fmin(kGammaTheta, fmin(kGammaPhi * thk / (-gd), sw_a));
+      }
+      sw_set = true;
+    };
+    constexpr bool kSwInSearch = Model::kEvalInSearch && !Model::kSOC;
+    if constexpr (!kSwInSearch) switching();
+    double Lt0 = 0.0;        // (kEvalInSearch) this lane's barrier log-sum at the first trial point
+    bool acc0 = false;       // accepted at the first trial of the filter line search
     if constexpr (!Model::kSOC) {
     for (int ls = 0; ls < 80; ++ls) {
       if (!__any(searching)) break;
@@ -1738,6 +1757,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
           STAMP(9);  // diagnostic: the trial's evaluation accumulates into phase 9
 #endif
           eval_at(zt, lt);
+          if constexpr (kSwInSearch) switching();
 #ifdef MPCX_STAMP_EVAL
           STAMP(6);
 #endif
@@ -1761,7 +1781,9 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
 #pragma unroll
           for (int i = 0; i < NX; ++i) tht_l += fabs(x0[i] - zt[i]);
       }
-      pht_l -= mu * barrier_logsum<NZ>(zt, lb, ub, hL, hU);
+      const double Lt = barrier_logsum<NZ>(zt, lb, ub, hL, hU);
+      if (ls == 0) Lt0 = Lt;
+      pht_l -= mu * Lt;
       double tp_[2] = {tht_l, pht_l};
       greduce_n<G, 0, 0>(tp_, xw);
       const double tht = tp_[0], pht = tp_[1];
@@ -1792,6 +1814,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
           accepted = true;
           ftype = ft;
           trial_fresh = Model::kEvalInSearch && ls == 0;
+          acc0 = ls == 0;
           if (ft) DIAG(7);
         } else {
           DIAG(2);
@@ -1824,6 +1847,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
           DIAG(12);
         }
         if (__any(go)) {
+          if (!sw_set) switching();  // (a soft phase skips the filter search)
           const double as = fmin(amax, az);
           double zt[NZ], lt[NX];
 #pragma unroll
@@ -1916,6 +1940,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
             if (accepted) {
               alpha = az = as;  // primal and dual variables take the same step
               trial_fresh = true;
+              acc0 = false;
             }
           }
         }
@@ -2243,6 +2268,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
           W(S + RestoWs::sGD) = gd;
           W(S + RestoWs::sAMAX) = amax;
           W(S + RestoWs::sAZ) = az;
+          if (!sw_set) switching();
           W(S + RestoWs::sSWA) = sw_a;
           W(S + RestoWs::sACCNOW) = acceptable_now ? 1.0 : 0.0;
           W(S + RestoWs::sSOFTTRIED) = soft_tried ? 1.0 : 0.0;
@@ -2300,6 +2326,8 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
 #pragma unroll
       for (int i = 0; i < NX; ++i) lam[i] = fma(alpha, dlam[i], lam[i]);
       fresh = trial_fresh;
+      lz_ok = acc0;  // z is the first trial point: its log-sum is Lt0
+      Lz = Lt0;
 #pragma unroll
       for (int i = 0; i < NZ; ++i) {
         if (hL[i]) {

@@ -75,7 +75,9 @@ def parse(lines):
                 cur["depth"] = int(d.group(1)) if d else cur["depth"]
                 cur["header"] = cur["label"].lstrip(".L")
             continue
-        cur["ins"].append(s.split()[0])
+        mn = s.split()[0]
+        st = re.search(r"stamp (\d+)", s) if mn == "s_memtime" else None
+        cur["ins"].append(f"s_memtime#{st.group(1)}" if st else mn)
     blocks.append(cur)
     return blocks
 
@@ -84,9 +86,12 @@ def budget(blocks, trips):
     phases, cur = [], None
     for b in blocks:
         for mn in b["ins"]:
-            if mn == "s_memtime" or cur is None:
-                cur = {"loops": {}, "straight": {}}
+            if mn.startswith("s_memtime") or cur is None:
+                # a stamp build labels each s_memtime with the phase it opens (kernels.h STAMP)
+                cur = {"loops": {}, "straight": {}, "phase": int(mn.split("#")[1]) if "#" in mn else None}
                 phases.append(cur)
+                if mn.startswith("s_memtime"):
+                    mn = "s_memtime"
             key = "straight" if b["depth"] <= 1 else "loops"
             tgt = cur["straight"] if key == "straight" else cur["loops"].setdefault(f"{b['header']}@{b['depth']}", {})
             c = classify(mn)
@@ -98,7 +103,7 @@ def budget(blocks, trips):
             t = trips.get(name.split("@")[0], 1)
             for c, n in cnt.items():
                 dyn[c] = dyn.get(c, 0) + t * n
-        out.append({"region": i, "straight": p["straight"], "loops": p["loops"],
+        out.append({"region": i, "phase": p["phase"], "straight": p["straight"], "loops": p["loops"],
                     "dynamic_estimate": dyn, "valu": dyn.get("valu_f64", 0) + dyn.get("valu_other", 0)})
     return out
 
