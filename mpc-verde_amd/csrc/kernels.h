@@ -50,7 +50,7 @@ constexpr int kDiag = 15;  // counters per instance
   do {                                                                          \
     __builtin_amdgcn_sched_barrier(0);                                          \
     unsigned long long t_;                                                      \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    asm volatile("s_memtime %0 ; stamp " #p "\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
     __builtin_amdgcn_sched_barrier(0);                                          \
     st_acc[st_ph] += t_ - st_last;                                              \
     st_last = t_;                                                               \
