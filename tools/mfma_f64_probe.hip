@@ -93,6 +93,40 @@ __global__ void latfma(double* out, long long* cyc, int n) {
   if (l == 0) *cyc = t1 - t0;
 }
 
+// issue cost of cross-lane moves of a double: 8 independent DPP row shifts (2 x v_mov_b32_dpp
+// each) or v_permlane32_swap pairs per step
+template <int KIND>
+__global__ void xlane(double* out, long long* cyc, int n) {
+  const int l = threadIdx.x;
+  double c[8];
+  for (int j = 0; j < 8; ++j) c[j] = 1e-3 * (l + j);
+  const long long t0 = __builtin_readcyclecounter();
+  for (int i = 0; i < n; i += 2) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const long long b = __double_as_longlong(c[j]);
+        int lo = (int)(b & 0xffffffffLL), hi = (int)(b >> 32);
+        if (KIND == 0) {
+          lo = __builtin_amdgcn_mov_dpp(lo, 0x111, 0xf, 0xf, true);
+          hi = __builtin_amdgcn_mov_dpp(hi, 0x111, 0xf, 0xf, true);
+        } else {
+          const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+          const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+          lo = a[0];
+          hi = h[0];
+        }
+        c[j] = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+      }
+  }
+  const long long t1 = __builtin_readcyclecounter();
+  double t = 0;
+  for (int j = 0; j < 8; ++j) t += c[j];
+  out[l] = t;
+  if (l == 0) *cyc = (t1 - t0) / 8;  // per double moved
+}
+
 // v_rcp_f64 and its Newton refinements: out[3 i + m] = m Newton steps from v_rcp_f64 of x[i]
 __global__ void rcp_probe(const double* x, double* out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -164,6 +198,8 @@ int main() {
   if (run(lat16<1>, "lat16_d_to_b", false)) return 1;
   if (run(latfma, "fma_f64_dep", false)) return 1;
   if (run(indfma, "fma_f64_indep_issue", false)) return 1;
+  if (run(xlane<0>, "dpp_row_shift_per_double", false)) return 1;
+  if (run(xlane<1>, "permlane32_swap_per_double", false)) return 1;
   // relative error of v_rcp_f64 with 0 / 1 / 2 Newton steps over 2^20 inputs spread over 1e-12..1e12
   {
     const int m = 1 << 20;
