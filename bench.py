@@ -22,7 +22,7 @@ IPM iteration of one instance needs -- per-node evaluation and Riccati step
 measured by tools/flop_probe.py, profiles/r04_flop_probe.json, plus the IPM's
 vector work counted in ipm_vector_flops; DESIGN.md §6 -- x the launch's
 instance-iterations) / the launch's HIP-event time / the FP64 vector peak, with
-the issued FP64 lane-flops of profiles/r03_solve_kernel_pmc.json beside it while
+the issued FP64 lane-flops of profiles/r04_solve_kernel_pmc.json beside it while
 that record matches the library's source hash.  `roofline_sweep` describes the
 RK4 + Jacobian sweep kernel (rk4_sens, the HBM-streaming kernel of SURVEY.md
 §8(d)) at B = 2^19, N = 20.  `cpu_baseline` times the C++ CPU oracle
@@ -46,7 +46,7 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # FP64 vector (VALU) peak: AMD's MI355X spec, half the FP32 vector peak of 157.3 TF/s
 # (MI355X_MICROARCH.md); the solve kernel issues scalar-per-lane FP64 FMAs, no MFMA
 PEAK_FP64_TFLOPS = 78.6
-SOLVE_PMC = os.path.join("profiles", "r03_solve_kernel_pmc.json")
+SOLVE_PMC = os.path.join("profiles", "r04_solve_kernel_pmc.json")
 SWEEP_BYTES_PER_STAGE = 256  # read x_k,u_k,x_{k+1} (64 B) + write c,q,A,B,grad q (192 B)
 SWEEP_BYTES_PER_INSTANCE = 48  # P
 
