@@ -111,6 +111,9 @@ __global__ void xlane(double* out, long long* cyc, int n) {
         if (KIND == 0) {
           lo = __builtin_amdgcn_mov_dpp(lo, 0x111, 0xf, 0xf, true);
           hi = __builtin_amdgcn_mov_dpp(hi, 0x111, 0xf, 0xf, true);
+        } else if (KIND == 2) {  // ds_bpermute from lane ^ 32 (the LDS crossbar, no LDS memory)
+          lo = __builtin_amdgcn_ds_bpermute((l ^ 32) << 2, lo);
+          hi = __builtin_amdgcn_ds_bpermute((l ^ 32) << 2, hi);
         } else {
           const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
           const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
@@ -200,6 +203,7 @@ int main() {
   if (run(indfma, "fma_f64_indep_issue", false)) return 1;
   if (run(xlane<0>, "dpp_row_shift_per_double", false)) return 1;
   if (run(xlane<1>, "permlane32_swap_per_double", false)) return 1;
+  if (run(xlane<2>, "ds_bpermute_xor32_per_double", false)) return 1;
   // relative error of v_rcp_f64 with 0 / 1 / 2 Newton steps over 2^20 inputs spread over 1e-12..1e12
   {
     const int m = 1 << 20;
