@@ -228,29 +228,6 @@ def _cold(P, N, nlp_ref):
     return nlp_ref.join_w(X, np.zeros((P.shape[0], N, 2)))
 
 
-CFG_KERNEL = {2: "UnicycleFreeModel", 3: "UnicycleScanModel", 4: "LinearModel<4, 1>", 5: "LinearModel<5, 1>"}
-VARIANT_KERNEL = {"kin_bicycle": "KinBicycle", "dyn_bicycle": "DynBicycle", "cartpole": "CartPole"}
-
-
-REPLICATED = ("UnicycleFreeModel", "UnicycleModel")  # models.h kReplicate
-
-
-def kernel_group(kname, N, B, n_simd, policy=0):
-    """(G, R) of the solve kernel instantiation the launch picks (kernels.h launch_solve_model): a
-    32-lane group widened to a wave runs replicated (R = 2) for the models that have it."""
-    G = group_size(N, B, n_simd, policy)
-    if kname in REPLICATED and G == 64 and group_size(N, B, n_simd, 1) == 32:
-        return 32, 2
-    return G, 1
-
-
-def group_size(N, B, n_simd, policy=0):
-    """Lanes per instance of the solve launch (csrc/solver.h solve_group_size)."""
-    G = 16 if N < 16 else 32 if N < 32 else 64 if N < 64 else 128 if N < 128 else 256
-    if policy == 0:
-        while G < 64 and B * G * 2 <= 64 * n_simd:
-            G *= 2
-    return G
 
 
 def usable_cpus():
@@ -324,7 +301,7 @@ def algorithmic_flops_per_iteration(key, ocp, N):
             "riccati_source": f"{FLOP_PROBE}: riccati {rk}", "bound_sides_per_node": nbs}, None
 
 
-def load_solve_pmc(kernel_substr, G, R=1):
+def load_solve_pmc(kernel):
     """The solve kernel's record in the committed PMC characterisation, if it was measured on
     the library built from the sources in this tree (else (None, reason): a stale record is
     never used)."""
@@ -338,13 +315,13 @@ def load_solve_pmc(kernel_substr, G, R=1):
     have, want = d.get("_meta", {}).get("mpcx_source_hash"), _lib.source_hash()
     if have is None or have != want:
         return None, f"stale: {SOLVE_PMC} measured on sources {have}, this tree is {want}"
-    for k, v in d.items():
-        if kernel_substr in k and f", {G}, false, {R}>" in k and v.get("f64_lane_flops_per_group_iteration"):
-            return (k, v), None
-    return None, f"no record for {kernel_substr} G={G} R={R} in {SOLVE_PMC}"
+    v = d.get(kernel)
+    if v and v.get("f64_lane_flops_per_group_iteration"):
+        return (kernel, v), None
+    return None, f"no record for {kernel} in {SOLVE_PMC}"
 
 
-def solve_roofline(kernel_substr, G, algo, group_iters, ms, R=1):
+def solve_roofline(kernel, algo, group_iters, ms):
     """Roofline entry of the fused solve kernel: algorithmic FP64 flops of the launch's IPM
     iterations / the launch's HIP-event time / the FP64 vector peak, with the issued FP64
     lane-flops of the committed PMC characterisation beside it (when current)."""
@@ -352,7 +329,7 @@ def solve_roofline(kernel_substr, G, algo, group_iters, ms, R=1):
         return None
     fl = algo["per_iteration"] * group_iters
     ach = fl / (ms * 1e-3) / 1e12
-    r = {"kernel": f"solve_kernel<{kernel_substr}..., G={G}" + (f" x{R} replicas" if R > 1 else "") + ">",
+    r = {"kernel": kernel,
          "bound": "valu", "achieved": round(ach, 4),
          "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 5), "traffic": None,
          "launch_ms": round(ms, 4), "group_iterations_per_launch": int(group_iters),
@@ -362,7 +339,7 @@ def solve_roofline(kernel_substr, G, algo, group_iters, ms, R=1):
          "algorithmic_flops_per_launch": fl,
          "note": "the kernel is bound by the issue of each instance's serial chains (one wave per SIMD), "
                  "not by HBM (traffic = its inputs/outputs, see solve_kernel.hbm_frac) nor by FP64 throughput"}
-    pmc, why = load_solve_pmc(kernel_substr, G, R)
+    pmc, why = load_solve_pmc(kernel)
     if pmc is None:
         r["issued"] = why
     else:
@@ -678,13 +655,11 @@ def main():
 
     # the dominant kernel of the timed region: the multi-step solve launch (async mode; HIP
     # events on the launch stream) or the mean single-step launch (lock-step latency run)
-    n_simd = 4 * torch.cuda.get_device_properties(local).multi_processor_count
-    kname = VARIANT_KERNEL[variant] if variant else CFG_KERNEL[cfg]
-    G, Rrep = kernel_group(kname, N, B, n_simd, solver.group_policy)
+    G, Rrep, kname = solver._h.launch_shape(B)  # the instantiation the library launches (mpcx_launch_shape)
     run_ms = res["run_ms"]
     run_iters = int(iters_hist.sum().item()) if args.mode == "async" else int(lk_it.sum().item())
     algo, why_not = algorithmic_flops_per_iteration(variant or cfg, ocp, N)
-    roof_solve = solve_roofline(kname, G, algo, run_iters, run_ms, Rrep) if rank == 0 else None
+    roof_solve = solve_roofline(kname, algo, run_iters, run_ms) if rank == 0 else None
     if rank == 0 and roof_solve is None:
         roof_solve = {"kernel": kname, "unavailable": why_not or "no timed iterations"}
 

@@ -102,7 +102,8 @@ typedef struct mpcx_spec {
   int32_t max_iter;     /* IPOPT max_iter (:190) */
   int32_t device;       /* HIP device ordinal */
   int32_t group_policy; /* lanes per instance: 0 = widen (up to 64) while the batch leaves SIMDs idle,
-                           1 = the smallest power of two >= N+1 (same results either way) */
+                           1 = the smallest power of two >= N+1 (the same bits either way; see
+                           mpcx_launch_shape) */
   double T;             /* sampling time (:31) */
   double tol;           /* IPOPT tol (default 1e-8) */
   double Q[8];          /* diagonal state weights (:78-83) */
@@ -158,11 +159,10 @@ const char* mpcx_source_hash(void);
  *   instances) or >= the batch size (row b = instance b; LTV schedules).
  * Call before solving; may be called again (e.g. per closed-loop step).
  * Reproducibility: with shared tables whose stages end in a decoupled suffix (B = 0, no x-u
- * weight; the move-blocked cart-pole QP), a launch that finds the suffix's value functions
- * cached by an earlier launch of this handle sums the suffix's linear part as a log-depth scan,
- * a fresh handle's first factorisation in chain order: the same solve then agrees to rounding
- * (~1e-12 relative) and in iteration counts, not bit for bit, across the two cache states.
- * Launches in the same cache state are bit-identical. */
+ * weight; the move-blocked cart-pole QP), a launch may find the suffix's value functions cached
+ * by an earlier launch of this handle; a factorisation that computes them afresh is redone on the
+ * path the cached ones take, so results are bit-identical whatever the cache state (fresh handle,
+ * cached handle, a later step of a multi-step launch). */
 int mpcx_set_linear_model(mpcx_handle* h, int32_t n_tab, const double* A, const double* B, const double* c,
                           const double* W, const int32_t* tab, int32_t tab_rows);
 
@@ -175,6 +175,28 @@ int mpcx_set_linear_tab_dev(mpcx_handle* h, const int32_t* d_tab, int32_t tab_ro
 
 /* n_w, n_g, n_p of the NLP described by the handle. */
 int mpcx_dims(const mpcx_handle* h, int32_t* n_w, int32_t* n_g, int32_t* n_p);
+
+/* Diagnostic environment knobs (A/B of two code paths; never needed in production):
+ *   MPCX_DEC_SUFFIX=0           read by mpcx_set_linear_model: no decoupled-suffix reuse (the full Riccati
+ *                               recursion at every factorisation; with it, config 5 at N >= 64 sums
+ *                               the suffix's vector part in chain order: ~1e-12 relative, same
+ *                               iteration counts)
+ *   MPCX_UNICYCLE_SCAN_MIN_N=n  read once per process: the unicycle horizon from which the Riccati recursion runs as
+ *                               the log-depth scan (default 25; 256 = never; ~1e-12 relative)
+ *
+ * The solve kernel a batch of B instances runs on this handle's device (no device work; no
+ * reference counterpart -- it names what the profiler will show):
+ *   lanes     lanes per instance group G (16, 32, 64, 128, 256; > 64 = one workgroup per instance)
+ *   replicas  1, or 2 when a batch too small to give every SIMD a wave widens a 32-lane group to
+ *             a wave and holds it twice, one replica per half-wave (group_policy 0)
+ *   kernel    the kernel's demangled name as rocprofv3 prints it (may be NULL), e.g.
+ *             "void mpcx::solve_kernel<mpcx::UnicycleFreeModel, 32, false, 2>(mpcx::SolveArgs)";
+ *             kernel_len = buffer size (EINVAL if too small)
+ * Batch-size dependence of the results: NONE.  Every group variant (narrow, widened, replicated,
+ * multi-wave) gives an instance the same bits, whatever batch, group_policy or device (SIMD count)
+ * it is solved with, so a global batch sharded over ranks returns what one device returns. */
+int mpcx_launch_shape(const mpcx_handle* h, int32_t B, int32_t* lanes, int32_t* replicas, char* kernel,
+                      int32_t kernel_len);
 
 /* Batched NLP solve (host pointers, synchronous).
  *   P      B x n_p parameters (layout per spec.param_layout)

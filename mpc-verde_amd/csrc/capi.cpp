@@ -550,6 +550,26 @@ static mpcx::SolveArgs make_args(const mpcx_handle* h, int B, const double* P, c
   return a;
 }
 
+int mpcx_launch_shape(const mpcx_handle* h, int32_t B, int32_t* lanes, int32_t* replicas, char* kernel,
+                      int32_t kernel_len) {
+  if (!h) return fail(MPCX_EINVAL, "null handle");
+  if (B < 1) return fail(MPCX_EINVAL, "B < 1");
+  if (kernel && kernel_len < 1) return fail(MPCX_EINVAL, "kernel_len < 1");
+  const mpcx::SolveArgs a = make_args(h, B, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                      nullptr, nullptr, nullptr, nullptr);
+  int G = 0, R = 0;
+  const char* model = nullptr;
+  if (mpcx::solve_shape(a, &G, &R, &model) != hipSuccess || !model) return fail(MPCX_EINVAL, "no kernel for this model");
+  if (lanes) *lanes = G;
+  if (replicas) *replicas = R;
+  if (kernel) {
+    const int n = snprintf(kernel, (size_t)kernel_len, "void mpcx::solve_kernel<%s, %d, false, %d>(mpcx::SolveArgs)",
+                           model, G, R);
+    if (n < 0 || n >= kernel_len) return fail(MPCX_EINVAL, "kernel name buffer too small");
+  }
+  return 0;
+}
+
 // launch the solve with the restoration workspace of the model (grown on demand; freed only
 // after the device is idle, since a queued launch may still use it)
 static int solve_launch(mpcx_handle* h, mpcx::SolveArgs& a, hipStream_t stream) {

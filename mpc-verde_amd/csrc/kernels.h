@@ -236,16 +236,6 @@ struct LdsCol {
   __device__ __forceinline__ void relaunder() { asm volatile("" : "+v"(off)); }
 };
 
-// Model::kReplicate if the model declares it: a 32-lane group may run replicated (R = 2, below)
-template <class M, class = void>
-struct ReplicateOf {
-  static constexpr bool value = false;
-};
-template <class M>
-struct ReplicateOf<M, std::void_t<decltype(M::kReplicate)>> {
-  static constexpr bool value = M::kReplicate;
-};
-
 // R = 2 (replicated groups, G = 32): a batch too small to give every SIMD a wave runs one
 // instance per wave with its lane group held TWICE, in the wave's two 32-lane halves (replica rho
 // = lane / 32).  Both replicas compute the same bits (every collective is a 32-lane group
@@ -270,6 +260,14 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   __shared__ double sbuf[Model::kParallelRiccati ? RElem<NX>::NE * kSBS : 1];
   // LDS cache of the ODE models' transcendental values across their derivative passes (ode.h)
   __shared__ double tcache[Model::kTrigSlots > 0 ? Model::kTrigSlots * kSBS : 1];
+  // the unicycle's narrow 32-lane groups (models.h stage_derivs): the lower half of the
+  // evaluation's moment sums waits here while the upper half is summed, instead of in registers
+#ifdef MPCX_EXP_LO_LDS
+  constexpr bool kLoStash = ReplicateOf<Model>::value && G == 32 && R == 1;
+#else
+  constexpr bool kLoStash = false;
+#endif
+  __shared__ double lostash[kLoStash ? kUniMoments * kSBS : 1];
   // the decoupled suffix's vector scan (multi-wave groups): two NX-double buffers per thread, then
   // the matrix powers (A^T)^(j 4^l), j = 1..3, l < 5, kept for the launch (table index pow_tab)
   __shared__ double dscan[DecSuffixOf<Model>::value && G > 64 ? 2 * NX * kSBS + 15 * NX * NX : 1];
@@ -311,6 +309,10 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     ModelArgs m = model_args(a);
     if (Model::kTrigSlots > 0) {
       m.tc = tcache + threadIdx.x;
+      m.tc_stride = kSBS;
+    }
+    if (kLoStash) {
+      m.tc = lostash + threadIdx.x;
       m.tc_stride = kSBS;
     }
     return m;
@@ -491,7 +493,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     if constexpr (R > 1)  // the replicas split the evaluation's sequential RK4 substeps
       Model::derivs_rep(ma, ctx, ze, ln, fs, xf, qv, A, Bm, gq, Hs, rho);
     else
-      Model::derivs(ma, ctx, ze, ln, fs, xf, qv, A, Bm, gq, Hs);
+      stage_derivs<Model, G>(ma, ctx, ze, ln, fs, xf, qv, A, Bm, gq, Hs);
     const double m = hasU ? 1.0 : 0.0, mx = (hasU && k > 0) ? 1.0 : 0.0;  // no x-gradient at X_0
     qv *= m;
     if constexpr (!Model::kTableHess)
@@ -1057,6 +1059,8 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     bool failed = false;
     bool first = true;
     Fac<NX, NU> fac = {};
+    // decoupled suffix: this factorisation starts without stored suffix value functions
+    const bool fresh_fac = !pcv;
     for (int attempt = 0; attempt < 64; ++attempt) {
       if (!__any(need)) break;
       STAMP_SUB(10);
@@ -1454,6 +1458,17 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
 #pragma unroll
       for (int i = 0; i < NX; ++i) pk[i] = p[i];
       const bool ok = gall<G, G * R>(okl, xw);
+      // Decoupled suffix of a multi-wave group (G > 64): the reused path sums the suffix's vector
+      // part by the log-depth scan, the full recursion in chain order.  A fresh delta = 0
+      // factorisation has just stored the suffix's P_k -- the bits the cross-launch cache would
+      // hold -- so it is redone on the reused path: an instance's result then does not depend on
+      // the cache state (a fresh handle, an earlier launch's cache, a step of a multi-step launch)
+      if constexpr (kDec && G > 64) {
+        if (need && ok && !pcv && delta == 0.0 && kb < N && pcache_ok(fs)) {  // block-uniform
+          pcv = true;
+          continue;
+        }
+      }
       // IPOPT inertia correction (Algorithm IC)
       if (need) {
         if (ok) {
@@ -1478,11 +1493,10 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
       its = it;
     }
     if constexpr (kDec) {
-      const bool fresh = !pcv;
       pcv = !failed && delta == 0.0;  // Pk now holds a delta = 0 factorisation
       // publish it for later launches (every writer stores the same bits; readers accept only
       // the header of an earlier launch, so a half-written cache is never read)
-      if (fresh && pcv && pcache_ok(fs)) {
+      if (fresh_fac && pcv && pcache_ok(fs)) {
         if (k >= kb && k <= N)
 #pragma unroll
           for (int i = 0; i < NP; ++i) a.pcache[(size_t)k * NP + i] = Pk[i];
@@ -2515,6 +2529,20 @@ __global__ void constraints_kernel(SolveArgs a, const double* __restrict__ W, do
 }
 
 // ---- launch helpers (called from capi.cpp) -----------------------------------
+// The solve kernel instantiation a launch picks: G lanes per group, R replicas of it per wave.  A
+// 32-lane group widened to a wave runs replicated (R = 2) where the model has that instantiation;
+// the results are the same bits either way (models.h stage_derivs).
+template <class Model>
+static void solve_shape(const SolveArgs& a, int* G, int* R) {
+  *G = solve_group_size(a.N, a.B, a.n_simd, a.group_policy);
+  *R = 1;
+  if constexpr (ReplicateOf<Model>::value)
+    if (*G == 64 && solve_group_size(a.N, a.B, a.n_simd, 1) == 32) {
+      *G = 32;
+      *R = 2;
+    }
+}
+
 template <class Model>
 static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
   // lane group: the smallest power of two holding nodes 0..N; G > 64 spans G/64 waves.
@@ -2524,13 +2552,14 @@ static hipError_t launch_solve_model(const SolveArgs& a, hipStream_t stream) {
   // solves/s in multi-step launches).  spec.group_policy = 1 keeps the narrowest group.
   // (Measured and not adopted: collectives over the 32 lanes of config 2's nodes on the same
   // 64-lane grid -- no gain)
-  const int G = solve_group_size(a.N, a.B, a.n_simd, a.group_policy);
+  int Gk, R;
+  solve_shape<Model>(a, &Gk, &R);
+  const int G = Gk * R;  // lanes per instance on the grid
   const long threads = (long)a.B * G;
   const int bs = G > 64 ? G : 64;
   const int blocks = (int)((threads + bs - 1) / bs);
-  // a 32-lane group widened to a wave runs replicated (R = 2) where the model has that instantiation
   if constexpr (ReplicateOf<Model>::value)
-    if (G == 64 && solve_group_size(a.N, a.B, a.n_simd, 1) == 32) {
+    if (R == 2) {
       hipLaunchKernelGGL((solve_kernel<Model, 32, false, 2>), dim3(blocks), dim3(64), 0, stream, a);
       return hipGetLastError();
     }
@@ -2548,12 +2577,14 @@ static hipError_t launch_resume_model(const SolveArgs& a, hipStream_t stream) {
   if constexpr (!RestoOf<Model>::value) {
     return hipSuccess;
   } else {
-    const int G = solve_group_size(a.N, a.B, a.n_simd, a.group_policy);
+    int Gk, R;
+    solve_shape<Model>(a, &Gk, &R);
+    const int G = Gk * R;
     const long threads = (long)a.B * G;
     const int bs = G > 64 ? G : 64;
     const int blocks = (int)((threads + bs - 1) / bs);
     if constexpr (ReplicateOf<Model>::value)
-      if (G == 64 && solve_group_size(a.N, a.B, a.n_simd, 1) == 32) {
+      if (R == 2) {
         hipLaunchKernelGGL((solve_kernel<Model, 32, true, 2>), dim3(blocks), dim3(64), 0, stream, a);
         return hipGetLastError();
       }
@@ -2601,8 +2632,13 @@ static hipError_t launch_shift_model(const SolveArgs& a, double* P, const double
 #else
 #define MPCX_INSTANTIATE_DIAG(tag)
 #endif
-#define MPCX_INSTANTIATE(Model, tag)                                                                        \
+#define MPCX_INSTANTIATE(Model, tag, name)                                                                  \
   namespace mpcx {                                                                                          \
+  hipError_t solve_shape_##tag(const SolveArgs& a, int* G, int* R, const char** kname) {                     \
+    solve_shape<Model>(a, G, R);                                                                            \
+    *kname = name;                                                                                          \
+    return hipSuccess;                                                                                      \
+  }                                                                                                         \
   hipError_t launch_solve_##tag(const SolveArgs& a, hipStream_t s) { return launch_solve_model<Model>(a, s); } \
   hipError_t launch_resume_##tag(const SolveArgs& a, hipStream_t s) { return launch_resume_model<Model>(a, s); } \
   hipError_t launch_plant_##tag(const SolveArgs& a, const double* U, double* XF, double* QF, hipStream_t s) {   \

@@ -7,6 +7,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "riccati.h"
 #include "solver.h"
 #include "unicycle.h"
@@ -63,7 +65,16 @@ struct UnicycleModel {
   __device__ __forceinline__ static void derivs(const ModelArgs& a, const Ctx& c, const double* z, const double* ln, double fs,
                                 double* xf, double& q, double* A, double* Bm, double* g, double* H) {
     const double u2[2] = {z[3], z[4]};
-    uni_derivs_moments(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H);  // weighted moments (unicycle.h)
+    uni_derivs_moments<0>(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H);  // weighted moments (unicycle.h)
+  }
+  // the same with the moments summed in the replicated groups' two halves: the 32-lane groups,
+  // which a small batch runs replicated (stage_derivs below), so that a node's bits do not depend
+  // on the batch it is solved in (the lower half waits in the kernel's LDS column a.tc, if given)
+  __device__ __forceinline__ static void derivs_halves(const ModelArgs& a, const Ctx& c, const double* z,
+                                                       const double* ln, double fs, double* xf, double& q, double* A,
+                                                       double* Bm, double* g, double* H) {
+    const double u2[2] = {z[3], z[4]};
+    uni_derivs_moments<1>(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H, 0, a.tc, a.tc_stride);
   }
   // the same evaluation split between the two replicas of a replicated lane group (kernels.h R = 2;
   // every lane of the wave must call it)
@@ -205,5 +216,27 @@ struct LinearModel {
     q = acc;
   }
 };
+
+// Model::kReplicate if the model declares it: a 32-lane group may run replicated (kernels.h R = 2)
+template <class M, class = void>
+struct ReplicateOf {
+  static constexpr bool value = false;
+};
+template <class M>
+struct ReplicateOf<M, std::void_t<decltype(M::kReplicate)>> {
+  static constexpr bool value = M::kReplicate;
+};
+
+// The stage evaluation of a group of G lanes, one per node (R = 1).  Where the same group may
+// also run replicated -- a replicating model's 32-lane groups, widened to a wave when the batch
+// leaves SIMDs idle (solve_group_size) -- the moments are summed in the replicas' two halves, so an
+// instance gets the same bits whatever batch (and hence group variant) it is solved in.
+template <class Model, int G, class... Args>
+__device__ __forceinline__ void stage_derivs(Args&&... args) {
+  if constexpr (ReplicateOf<Model>::value && G == 32)
+    Model::derivs_halves(args...);
+  else
+    Model::derivs(args...);
+}
 
 }  // namespace mpcx

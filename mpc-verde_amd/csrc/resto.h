@@ -249,7 +249,7 @@ __device__ __forceinline__ void recover(RecIO& io, FilterLds<G>& filt, const Mod
     }
     double ze[NZ];
     stage_point(zz, ze);
-    Model::derivs(ma, ctx, ze, ln, fse, xf, qv, A, Bm, gq, Hs);
+    stage_derivs<Model, G>(ma, ctx, ze, ln, fse, xf, qv, A, Bm, gq, Hs);
     const double m = hasU ? 1.0 : 0.0, mx = (hasU && k > 0) ? 1.0 : 0.0;
     qv *= m;
 #pragma unroll

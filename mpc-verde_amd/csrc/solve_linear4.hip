@@ -4,4 +4,4 @@
 namespace mpcx {
 using Linear4x1 = LinearModel<4, 1>;
 }
-MPCX_INSTANTIATE(Linear4x1, linear4)
+MPCX_INSTANTIATE(Linear4x1, linear4, "mpcx::LinearModel<4, 1>")

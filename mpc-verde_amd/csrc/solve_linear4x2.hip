@@ -6,4 +6,4 @@
 namespace mpcx {
 using Linear4x2 = LinearModel<4, 2>;
 }
-MPCX_INSTANTIATE(Linear4x2, linear4x2)
+MPCX_INSTANTIATE(Linear4x2, linear4x2, "mpcx::LinearModel<4, 2>")

@@ -4,4 +4,4 @@
 namespace mpcx {
 using Linear5x1 = LinearModel<5, 1>;
 }
-MPCX_INSTANTIATE(Linear5x1, linear5)
+MPCX_INSTANTIATE(Linear5x1, linear5, "mpcx::LinearModel<5, 1>")

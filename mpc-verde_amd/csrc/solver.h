@@ -91,7 +91,7 @@ struct ModelArgs {
   LinTables lin;
   OdeParams op;
   int p_layout, N;
-  double* tc = nullptr;  // ODE models: this lane's slot 0 of the solve kernel's LDS value cache
+  double* tc = nullptr;  // this lane's slot 0 of an LDS column: the ODE models' value cache, the unicycle's moment stash
   int tc_stride = 0;     // slot stride (threads per block)
 };
 __host__ __device__ inline ModelArgs model_args(const SolveArgs& a) { return ModelArgs{a.sp, a.lin, a.op, a.p_layout, a.N}; }
@@ -141,6 +141,9 @@ __host__ __device__ constexpr int chain_ws_slots(int nx, int nu) {
 int resto_ws_slots(int model, int nx, int nu);
 
 hipError_t launch_solve(const SolveArgs& a, hipStream_t stream);
+// the solve kernel a launch with these arguments runs: G lanes per group, R replicas of the group per
+// wave, and the instantiation's model type ("mpcx::UnicycleFreeModel", ...)
+hipError_t solve_shape(const SolveArgs& a, int* G, int* R, const char** kname);
 // the resume launch of models with a restoration phase: continues the instances the solve
 // launch left at a failed line search (no-op for the others)
 hipError_t launch_resume(const SolveArgs& a, hipStream_t stream);

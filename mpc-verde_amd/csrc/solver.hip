@@ -99,6 +99,7 @@ int resto_ws_slots(int model, int nx, int nu) {
 #define MPCX_DECLARE(tag)                                                                                       \
   hipError_t launch_solve_##tag(const SolveArgs&, hipStream_t);                                                 \
   hipError_t launch_resume_##tag(const SolveArgs&, hipStream_t);                                                \
+  hipError_t solve_shape_##tag(const SolveArgs&, int*, int*, const char**);                                     \
   hipError_t launch_plant_##tag(const SolveArgs&, const double*, double*, double*, hipStream_t);                \
   hipError_t launch_constraints_##tag(const SolveArgs&, const double*, double*, hipStream_t);                    \
   hipError_t launch_shift_##tag(const SolveArgs&, double*, const double*, double*, const double*, double*,       \
@@ -149,6 +150,9 @@ static int unicycle_scan_min_n() {
 
 hipError_t launch_solve(const SolveArgs& a, hipStream_t stream) { MPCX_DISPATCH(a, launch_solve, a, stream); }
 hipError_t launch_resume(const SolveArgs& a, hipStream_t stream) { MPCX_DISPATCH(a, launch_resume, a, stream); }
+hipError_t solve_shape(const SolveArgs& a, int* G, int* R, const char** kname) {
+  MPCX_DISPATCH(a, solve_shape, a, G, R, kname);
+}
 hipError_t launch_plant(const SolveArgs& a, const double* U, double* XF, double* QF, hipStream_t stream) {
   MPCX_DISPATCH(a, launch_plant, a, U, XF, QF, stream);
 }

@@ -30,7 +30,7 @@ STATUS = {0: "Solve_Succeeded", 1: "Solved_To_Acceptable_Level", 2: "Maximum_Ite
 EXPORTS = ("mpcx_default_spec", "mpcx_create", "mpcx_destroy", "mpcx_last_error", "mpcx_dims", "mpcx_solve_batch",
            "mpcx_solve_batch_dev", "mpcx_plant_step", "mpcx_shift_dev", "mpcx_rk4_sens", "mpcx_rk4_sens_dev",
            "mpcx_set_linear_model", "mpcx_set_linear_tab_dev", "mpcx_step_dev", "mpcx_run_dev",
-           "mpcx_source_hash")
+           "mpcx_source_hash", "mpcx_launch_shape")
 STEP_COLD = 1
 STEP_PRIMAL_ONLY = 2
 
@@ -125,6 +125,7 @@ def load():
     lib.mpcx_destroy.restype = None
     lib.mpcx_last_error.restype = ctypes.c_char_p
     lib.mpcx_dims.argtypes = [H, ip, ip, ip]
+    lib.mpcx_launch_shape.argtypes = [H, ctypes.c_int32, ip, ip, ctypes.c_char_p, ctypes.c_int32]
     lib.mpcx_solve_batch.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, ip, ip]
     lib.mpcx_solve_batch_dev.argtypes = [H, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mpcx_plant_step.argtypes = [H, ctypes.c_int32, dp, dp, dp, dp]
@@ -194,6 +195,14 @@ class Handle:
         check(load().mpcx_set_linear_model(self._h, int(n_tab), dptr(A), dptr(B), dptr(c), dptr(Wp), iptr(tab),
                                            int(rows)))
         self._lin_refs = (A, B, c, Wp, tab)
+
+    def launch_shape(self, B):
+        """(lanes per group, replicas per wave, kernel name) of a B-instance solve launch
+        (mpcx_launch_shape: the instantiation rocprofv3 will name)."""
+        G, R = ctypes.c_int32(), ctypes.c_int32()
+        buf = ctypes.create_string_buffer(256)
+        check(load().mpcx_launch_shape(self._h, int(B), ctypes.byref(G), ctypes.byref(R), buf, len(buf)))
+        return G.value, R.value, buf.value.decode()
 
     @property
     def spec(self):

@@ -66,11 +66,15 @@ def _coll_device(device):
     return None if dist.get_backend() == "gloo" else device
 
 
-def init(backend: str):
+def init(backend: str, always: bool = False):
+    """Create the process group from the torch.distributed.run environment: for world_size > 1, or
+    at world_size 1 too when `always` (then the stats collectives below run through the backend --
+    RCCL with one rank -- instead of short-circuiting).  Call before any other HIP use of the
+    process (RCCL binds the rank's device)."""
     import torch.distributed as dist
 
     rank, world, _ = env()
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or always) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, world
@@ -233,7 +237,7 @@ def all_gather_stats(S_local, device=None):
     import torch
     import torch.distributed as dist
 
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not dist.is_initialized():
         return np.asarray(S_local)
     t = torch.as_tensor(np.ascontiguousarray(S_local), dtype=torch.float64)
     device = _coll_device(device)
@@ -248,7 +252,7 @@ def max_over_ranks(x: float, device=None):
     import torch
     import torch.distributed as dist
 
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not dist.is_initialized():
         return float(x)
     t = torch.tensor([x], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -1,0 +1,164 @@
+"""GPU: the BASELINE-named configs at their full per-GPU batch (BASELINE.json configs 3 and 5),
+the sizes the bench runs, not test-sized batches:
+
+* config 3 as named -- kinematic bicycle, circular reference, N = 30, B = 4096;
+* config 5 family -- the cart-pole QP of inverted_pendulum_single_shooting_mpctools.py:16,64 at
+  N = 100 (two-wave groups, decoupled suffix), B = 2048;
+* config 5 as named -- the cart-pole swing-up, N = 100, B = 2048 (the bench's multiple-shooting
+  closed loop, and the single-shooting formulation of the reference script cold).
+
+Each: every status <= 1; a 3-step multi-step launch (DeviceLoop.run, the bench's timed path)
+equals 3 lock-step launches bit for bit on the whole batch; and the C++ IPOPT restatement
+(oracle/ipm_ref.cpp) or the pinned QP oracle agrees on a strided sample of 64 instances.
+PARITY UNPINNED for the ODE models (no reference outputs exist); the cart-pole QP oracle is pinned
+to invertpend_data_py.xlsx (tests/test_linear_cpu.py).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+U_TOL = 1e-6
+SAMPLE = 64
+
+
+@pytest.fixture(scope="module")
+def mpcx():
+    import mpcx as m
+
+    m._lib.load()
+    return m
+
+
+@pytest.fixture(scope="module")
+def C():
+    from oracle import ipm_ref
+
+    ipm_ref.lib()
+    return ipm_ref
+
+
+def u_err(wa, wb, nx, nz, N):
+    iu = np.concatenate([nx + nz * k + np.arange(nz - nx) for k in range(N)])
+    ua, ub = wa[:, iu], wb[:, iu]
+    return np.max(np.abs(ua - ub), axis=1) / np.maximum(np.max(np.abs(ub), axis=1), 1.0)
+
+
+def run_vs_lockstep(solver, P0, K, refs=None):
+    """K lock-step launches (step()) against ONE K-step launch (run()), from the same cold start:
+    per-step statuses / iterations and the final state, bit for bit.  refs: (K, B, n_p - nx)
+    device tensor of per-step stage references, or None."""
+    import torch
+
+    from mpcx.device import DeviceLoop
+
+    lock, run = DeviceLoop(solver, P0), DeviceLoop(solver, P0)
+    st_l, it_l = [], []
+    for t in range(K):
+        if refs is not None:
+            lock.set_stage_refs(refs[t])
+        lock.step()
+        torch.cuda.synchronize()
+        st_l.append(lock.status.cpu().numpy().copy())
+        it_l.append(lock.iters.cpu().numpy().copy())
+    Pseq = None
+    if refs is not None:
+        Pseq = torch.zeros((K,) + tuple(run.P.shape), dtype=torch.float64, device=run.P.device)
+        Pseq[:, :, run.P.shape[1] - refs.shape[2]:] = refs
+        run.set_stage_refs(refs[0])
+    st_r, it_r = run.run(K, Pseq=Pseq)
+    torch.cuda.synchronize()
+    st_l, it_l = np.array(st_l), np.array(it_l)
+    np.testing.assert_array_equal(st_r.cpu().numpy(), st_l)
+    np.testing.assert_array_equal(it_r.cpu().numpy(), it_l)
+    names = ("w", "w0", "lam0", "lamx0", "f") if refs is not None else ("P", "w", "w0", "lam", "lamx", "f")
+    for n in names:
+        np.testing.assert_array_equal(getattr(run, n).cpu().numpy(), getattr(lock, n).cpu().numpy(), err_msg=n)
+    if refs is not None:  # run keeps the step-0 references in P: compare x0
+        nx = run.P.shape[1] - refs.shape[2]
+        np.testing.assert_array_equal(run.P[:, :nx].cpu().numpy(), lock.P[:, :nx].cpu().numpy())
+    assert np.all(st_l <= 1), np.unique(st_l, return_counts=True)
+    return st_l, it_l
+
+
+def oracle_sample(name, ocp, P, r, ref, idx, nx, nz, max_differ=0, max_iter_differ=0):
+    e = u_err(r["w"][idx], ref["w"], nx, nz, ocp.N)
+    n_u = int(np.sum(e > U_TOL))
+    n_it = int(np.sum(r["iters"][idx] != ref["iters"]))
+    print(f"{name}: {n_u} of {len(idx)} sampled optima and {n_it} iteration counts differ from the C++ oracle "
+          f"(max input difference {e.max():.2e})")
+    assert np.all(ref["status"] <= 1)
+    assert n_u <= max_differ and n_it <= max_iter_differ
+
+
+def test_config3_kin_bicycle_full_batch(mpcx, C):
+    """Config 3 as named: kinematic bicycle on the config-3 circle, N = 30, B = 4096."""
+    import torch
+
+    from mpcx import dist as mdist
+
+    N, B, K = 30, 4096, 3
+    ocp = mpcx.kinematic_bicycle_tracking(N=N)
+    tau0, P = mdist.config3_bicycle_inputs(0, B, N=N)
+    solver = mpcx.nlpsol("kin", "mi355x", ocp, {"ipopt": {"max_iter": 3000}})
+    r = solver.solve_batch(P)
+    assert np.all(r["status"] <= 1), np.unique(r["status"], return_counts=True)
+    idx = np.arange(0, B, B // SAMPLE)
+    ref = C.solve(ocp, P[idx], nthreads=0)
+    oracle_sample("config 3 kinematic bicycle N=30 B=4096", ocp, P, r, ref, idx, 3, 5)
+    refs = torch.from_numpy(np.stack([mpcx.ode.bicycle_circular_reference(tau0, t, N).reshape(B, -1)
+                                      for t in range(K)])).cuda()
+    run_vs_lockstep(solver, P, K, refs)
+
+
+def test_config5_pendulum_qp_full_batch(mpcx):
+    """Config 5 family: the cart-pole QP (u_prev augmentation, 5 free moves, 95 blocked), N = 100,
+    B = 2048 -- two-wave groups, the decoupled suffix scanned; the QP oracle on a strided sample."""
+    from mpcx import dist as mdist
+    from mpcx import lti
+    from oracle import nlp_ref
+
+    N, B, K = 100, 2048, 3
+    lin = lti.inverted_pendulum_qp(N=N)
+    x0 = mdist.config5_inputs(0, B)
+    P = lti.pendulum_params(lin, x0, 0.0)
+    solver = mpcx.nlpsol("pend", "mi355x", lin, {"ipopt": {"max_iter": 200}})
+    r = solver.solve_batch(P)
+    assert np.all(r["status"] == 0)
+    A, Bd = nlp_ref.pendulum_model()
+    worst = 0.0
+    for b in range(0, B, B // SAMPLE):
+        u_ref = nlp_ref.pendulum_qp_solve(x0[b], A, Bd, N=N, uprev=0.0)
+        u = r["w"][b, 5:5 + 6 * 5:6]
+        worst = max(worst, float(np.max(np.abs(u - u_ref)) / max(float(np.max(np.abs(u_ref))), 1.0)))
+    print(f"config 5 QP N=100 B=2048: max sampled input difference from the pinned QP oracle {worst:.2e}")
+    assert worst <= U_TOL
+    run_vs_lockstep(solver, P, K)
+
+
+def test_config5_swingup_full_batch(mpcx, C):
+    """Config 5 as named: cart-pole swing-up from hanging starts, N = 100, B = 2048 -- the bench's
+    closed loop (multiple shooting), and the single-shooting formulation cold with the oracle on a
+    strided sample."""
+    from mpcx import dist as mdist
+    from oracle import ode_ref
+
+    N, B, K = 100, 2048, 3
+    P = mdist.config5_swingup_inputs(0, B)
+    ocp = mpcx.cartpole_swingup(N=N)
+    solver = mpcx.nlpsol("cp", "mi355x", ocp, {"ipopt": {"max_iter": 3000}})
+    r = solver.solve_batch(P)
+    assert np.all(r["status"] <= 1), np.unique(r["status"], return_counts=True)
+    idx = np.arange(0, B, B // SAMPLE)
+    ref = C.solve(ocp, P[idx], nthreads=0)
+    oracle_sample("config 5 swing-up (multiple shooting) N=100 B=2048", ocp, P, r, ref, idx, 4, 5)
+    run_vs_lockstep(solver, P, K)
+    # the reference script's formulation: single shooting (decision U, X the rollout)
+    ss = mpcx.cartpole_swingup(N=N, formulation="single_shooting")
+    pr = ode_ref.Problem(ss)
+    U0 = np.zeros((N, 1))
+    w0 = np.stack([pr.join_w(pr.rollout(U0, P[b][:4]), U0) for b in range(B)])
+    rs = mpcx.nlpsol("ss", "mi355x", ss, {"ipopt": {"max_iter": 3000}}).solve_batch(P, w0)
+    assert np.all(rs["status"] <= 1), np.unique(rs["status"], return_counts=True)
+    refs = C.solve(ss, P[idx], w0=w0[idx], nthreads=0)
+    oracle_sample("config 5 swing-up (single shooting) N=100 B=2048", ss, P, rs, refs, idx, 4, 5)

@@ -225,11 +225,12 @@ def test_pendulum_long_horizon_multiwave(mpcx, R, N):
     for b in range(B):
         u_ref = R.pendulum_qp_solve(x[b], A, Bd, N=N, uprev=up[b])
         assert rel(r["w"][b, 5:5 + 6 * 5:6], u_ref) <= U_TOL, b
-    # instances are independent: a ragged sub-batch gives bit-identical results (a fresh handle:
-    # a second launch of S would start from the suffix cache, whose scan sums in another order)
+    # instances are independent: a ragged sub-batch gives bit-identical results, on a fresh handle
+    # and on S, whose second launch starts from the suffix cache
     S2 = mpcx.nlpsol("pend", "mi355x", lin, {"ipopt": {"max_iter": 200}})
-    r2 = S2.solve_batch(lti.pendulum_params(lin, x[5:12], up[5:12]))
-    np.testing.assert_array_equal(r2["w"], r["w"][5:12])
+    for h in (S2, S):
+        r2 = h.solve_batch(lti.pendulum_params(lin, x[5:12], up[5:12]))
+        np.testing.assert_array_equal(r2["w"], r["w"][5:12])
 
 
 @pytest.mark.parametrize("N", [50, 100])
@@ -239,8 +240,9 @@ def test_pendulum_decoupled_suffix_same_bits(mpcx, R, N, monkeypatch):
     earlier one cached.  Same solution bits, multipliers and iteration counts as the full
     recursion (MPCX_DEC_SUFFIX=0), with and without the cache, and the LQ oracle's solution.
     At N = 100 (two-wave groups) the reused suffix runs as a log-depth vector scan (kernels.h,
-    "reused suffix as a log-depth scan"), whose sums associate differently: there the same iteration counts and a
-    solution within 1e-9 of the full recursion's."""
+    "reused suffix as a log-depth scan"), whose sums associate differently: there the same
+    iteration counts and a solution within 1e-9 of the full recursion's -- and the same bits with
+    and without the cache (a fresh factorisation is redone on the reused path)."""
     from mpcx import lti
 
     lin = lti.inverted_pendulum_qp(N=N)
@@ -259,6 +261,8 @@ def test_pendulum_decoupled_suffix_same_bits(mpcx, R, N, monkeypatch):
     # the first launch cached (capi SolveArgs::pcache): the same bits again
     a2 = S_fast.solve_batch(P)
     assert np.all(a["status"] == 0)
+    for n in ("w", "f", "lam_g", "lam_x", "iters", "status"):  # cache state: no effect on the bits
+        np.testing.assert_array_equal(a2[n], a[n], err_msg=n)
     for r in (a, a2):
         np.testing.assert_array_equal(r["iters"], b["iters"])
         if N < 64:
@@ -393,10 +397,9 @@ def test_pendulum_run_equals_lockstep_decoupled_suffix(mpcx, dec, monkeypatch):
     """The config-5 path as benchmarked: DeviceLoop.run(K) (one multi-step launch: warm duals,
     mu_init 1e-4, kb / pcv re-derived at every step boundary, two-wave groups at N = 100) against
     K lock-step launches, with the decoupled-suffix reuse on and off (MPCX_DEC_SUFFIX=0): the same
-    iterations and status at every step, and the same bits for w and the multipliers with the
-    reuse off; with it on, within 1e-9 (lock-step launches after the first start from the suffix
-    cache and take the vector scan at their first factorisation, where the steps of a multi-step
-    launch run the full recursion first; the two sum in different orders)."""
+    iterations, status and bits at every step.  With the reuse on, the lock-step launches after
+    the first start from the suffix cache, the steps of the multi-step launch from their own
+    fresh factorisation, which is redone on the reused path (kernels.h), so the bits agree."""
     import torch
     from mpcx import dist as mdist
     from mpcx import lti
@@ -420,20 +423,16 @@ def test_pendulum_run_equals_lockstep_decoupled_suffix(mpcx, dec, monkeypatch):
     assert np.all(np.array(st_l) == 0)
     for n in ("P", "w", "w0", "lam", "lamx", "f"):
         got, want = getattr(run, n).cpu().numpy(), getattr(lock, n).cpu().numpy()
-        if dec == "0":
-            np.testing.assert_array_equal(got, want, err_msg=n)
-        else:
-            assert close(got, want) <= 1e-9, n
+        np.testing.assert_array_equal(got, want, err_msg=n)
 
 
 def test_pendulum_suffix_cache_follows_table_changes(mpcx):
     """The decoupled suffix's P_k cached across launches (capi SolveArgs::pcache) belong to one
     table generation: after mpcx_set_linear_model with other weights (q), and after a schedule
     change that moves the free/blocked boundary (n_free), a handle that has cached the old
-    suffix gives the same result as a fresh handle of the new problem: the same iteration counts
-    and a solution within 1e-9 (not the same bits: the cached handle's first factorisation
-    already takes the suffix scan, the fresh handle's runs the full recursion; a stale cache
-    would give another problem's solution)."""
+    suffix gives the same result as a fresh handle of the new problem, bit for bit (the fresh
+    handle's first factorisation is redone on the reused path the cached handle takes; a stale
+    cache would give another problem's solution)."""
     from mpcx import lti
 
     N, B = 100, 64
@@ -448,7 +447,7 @@ def test_pendulum_suffix_cache_follows_table_changes(mpcx):
         r1 = S.solve_batch(P)
     ref1 = mpcx.nlpsol("pc1", "mi355x", lin1, {"ipopt": {"max_iter": 200}}).solve_batch(P)
     np.testing.assert_array_equal(r1["iters"], ref1["iters"])
-    assert close(r1["w"], ref1["w"]) <= 1e-9
+    np.testing.assert_array_equal(r1["w"], ref1["w"])
     for lin in (lin2, lin3):
         S.set_linear_model(lin)
         r = S.solve_batch(P)
@@ -456,7 +455,8 @@ def test_pendulum_suffix_cache_follows_table_changes(mpcx):
         ref = mpcx.nlpsol("pcf", "mi355x", lin, {"ipopt": {"max_iter": 200}}).solve_batch(P)
         assert np.all(ref["status"] == 0)
         for got in (r, r_again):
-            assert close(got["w"], ref["w"]) <= 1e-9
+            np.testing.assert_array_equal(got["w"], ref["w"])
+            np.testing.assert_array_equal(got["lam_g"], ref["lam_g"])
             np.testing.assert_array_equal(got["iters"], ref["iters"])
         assert np.max(np.abs(r["w"] - r1["w"])) > 1e-6  # the problems really differ
 

@@ -309,24 +309,75 @@ def test_horizons(mpcx, C, R, N):
 def test_group_policy_same_results(mpcx, N, B):
     """Lane-group widening (spec.group_policy 0, the default: up to one instance per wave while
     SIMDs would idle) and the narrowest group (policy 1: 4/2 instances per wave at N=10/20) give
-    the same results.  Widening a 16-lane group (N = 10) or running one multi-wave group adds exact
-    zeros / neutral values to every reduction: the same bits.  A 32-lane group widened to a wave
-    (N = 20) runs replicated (kernels.h R = 2), and its replicas split the stage evaluation's RK4
-    substeps, summing the quadrature moments in two halves: there the same statuses and iteration
-    counts and a solution within 1e-9 (relative) of the narrow group's.  Policy 1 is also how the
-    narrow-group code paths stay covered at test batch sizes."""
+    the same bits.  Widening a 16-lane group (N = 10) or running one multi-wave group adds exact
+    zeros / neutral values to every reduction.  A 32-lane group widened to a wave (N = 20) runs
+    replicated (kernels.h R = 2), its replicas splitting the stage evaluation's RK4 substeps; the
+    narrow 32-lane group sums the quadrature moments in the same two halves (models.h
+    stage_derivs), so it too gives the same bits.  Policy 1 is also how the narrow-group code
+    paths stay covered at test batch sizes."""
     ocp = mpcx.unicycle_point_to_point(N=N)
     P = config2_batch(B, seed=N + 1)
-    r0 = mpcx.nlpsol("s", "mi355x", ocp).solve_batch(P)
-    r1 = mpcx.nlpsol("s", "mi355x", ocp, {"group_policy": 1}).solve_batch(P)
+    s0 = mpcx.nlpsol("s", "mi355x", ocp)
+    s1 = mpcx.nlpsol("s", "mi355x", ocp, {"group_policy": 1})
+    if N == 20:  # the two policies do run different kernels here
+        assert s0._h.launch_shape(B)[:2] == (32, 2) and s1._h.launch_shape(B)[:2] == (32, 1)
+    r0, r1 = s0.solve_batch(P), s1.solve_batch(P)
     assert np.all(r0["status"] == 0)
-    replicated = 16 <= N < 32
     for n in ("w", "f", "lam_g", "lam_x", "status", "iters"):
-        if replicated and n in ("w", "f", "lam_g", "lam_x"):
-            scale = np.maximum(np.max(np.abs(r1[n]), axis=-1, keepdims=True) if r1[n].ndim > 1 else np.abs(r1[n]), 1.0)
-            assert np.max(np.abs(r0[n] - r1[n]) / scale) <= 1e-9, n
-        else:
-            np.testing.assert_array_equal(r0[n], r1[n], err_msg=n)
+        np.testing.assert_array_equal(r0[n], r1[n], err_msg=n)
+
+
+def test_launch_shape_names_the_kernel(mpcx):
+    """mpcx_launch_shape reports the instantiation a launch runs (what bench.py looks up in the
+    PMC record and rocprofv3 prints): config 2's 1024 instances on a 1024-SIMD MI355X run
+    replicated 32-lane groups, one more instance tips the batch to the narrow groups."""
+    import torch
+
+    n_simd = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    h = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=20))._h
+    Bw = n_simd  # the largest batch that still widens 32-lane groups (B * 32 * 2 <= 64 * n_simd)
+    assert h.launch_shape(Bw) == (32, 2, "void mpcx::solve_kernel<mpcx::UnicycleFreeModel, 32, false, 2>"
+                                        "(mpcx::SolveArgs)")
+    assert h.launch_shape(Bw + 1)[:2] == (32, 1)
+    h10 = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=10))._h
+    assert h10.launch_shape(16)[:2] == (64, 1) and h10.launch_shape(100 * n_simd)[:2] == (16, 1)
+    h30 = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=30))._h  # scan model: never replicated
+    assert h30.launch_shape(16) == (64, 1, "void mpcx::solve_kernel<mpcx::UnicycleScanModel, 64, false, 1>"
+                                          "(mpcx::SolveArgs)")
+    hp = mpcx.nlpsol("s", "mi355x", mpcx.inverted_pendulum_qp(N=100))._h
+    assert hp.launch_shape(2048) == (128, 1, "void mpcx::solve_kernel<mpcx::LinearModel<5, 1>, 128, false, 1>"
+                                             "(mpcx::SolveArgs)")
+
+
+def test_instance_bits_do_not_depend_on_the_batch(mpcx):
+    """SURVEY.md §4 item 5 at the group-variant boundary: the same config-2 instances solved in a
+    batch of n_simd (1024 on MI355X: replicated 32-lane groups), inside a batch of 2 n_simd (narrow
+    groups) and inside n_simd + 1 (just across the widening threshold) give identical w, f, lambda,
+    statuses and iteration counts -- cold, and warm-started from the shifted solution."""
+    import torch
+
+    import bench
+    from mpcx import dist
+
+    n_simd = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    N, B = 20, n_simd
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=N))
+    assert solver._h.launch_shape(B)[1] == 2 and solver._h.launch_shape(B + 1)[1] == 1
+    P2 = dist.config2_inputs(0, 2 * B)
+    r_rep = solver.solve_batch(P2[:B])
+    for Bb in (2 * B, B + 1):
+        r_nar = solver.solve_batch(P2[:Bb])
+        for n in ("w", "f", "lam_g", "lam_x", "status", "iters"):
+            np.testing.assert_array_equal(r_rep[n], r_nar[n][:B], err_msg=f"{n} (B={Bb})")
+    # one warm-started closed-loop step later (IPOPT warm_start_init_point from shifted multipliers)
+    rn = solver.solve_batch(P2)
+    w0, l0, lx0 = bench.shift_np(rn["w"], N), bench.shift_lam_np(rn["lam_g"], N), bench.shift_lamx_np(rn["lam_x"], N)
+    Pn = P2.copy()
+    Pn[:, 0:3] = rn["w"][:, 3 + 2:3 + 2 + 3]  # x0 <- the predicted X_1
+    wa = solver.solve_batch(Pn[:B], w0=w0[:B], lam_g0=l0[:B], lam_x0=lx0[:B])
+    wb = solver.solve_batch(Pn, w0=w0, lam_g0=l0, lam_x0=lx0)
+    for n in ("w", "f", "lam_g", "lam_x", "status", "iters"):
+        np.testing.assert_array_equal(wa[n], wb[n][:B], err_msg=f"warm {n}")
 
 
 def test_max_iter_status(mpcx):
@@ -870,7 +921,9 @@ def test_bench_two_ranks_rehearsal(tmp_path):
     env = dict(os.environ, MPCX_FORCE_DEVICE="0", MPCX_DIST_BACKEND="gloo")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    B = 512
+    # B per rank = the SIMD count of the MI355X (1024): each rank's launches run replicated 32-lane
+    # groups, the single rank's 2B instances the narrow ones -- the weak-scaling case of the bench
+    B = 1024
     common = ["--steps", "3", "--warmup", "1", "--no-cpu", "--no-roofline", "--no-reference-warm-start"]
     flags = ["--gpus", "2", "--batch", str(B)] + common
     launched = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",

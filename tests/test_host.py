@@ -161,34 +161,16 @@ def test_filter_harness_builds_and_exports():
     assert lib.filter_check_capacity(8) == -1
 
 
-def test_bench_group_size_and_usable_cpus():
-    """bench.py's lane-group rule (used to find the solve kernel's PMC record for its roofline)
-    is csrc/solver.h solve_group_size, and its CPU count for the baseline is every CPU the
-    process may run on (affinity mask, capped by a cgroup quota), never OMP_NUM_THREADS."""
+def test_bench_usable_cpus():
+    """bench.py's CPU count for the baseline is every CPU the process may run on (affinity mask,
+    capped by a cgroup quota), never OMP_NUM_THREADS.  (The solve kernel whose PMC record the
+    roofline uses is named by the library itself, mpcx_launch_shape: tests/test_gpu_parity.py.)"""
     import importlib.util
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-
-    def cpp_rule(N, B, n_simd, policy):  # csrc/solver.h solve_group_size
-        G = 16 if N < 16 else 32 if N < 32 else 64 if N < 64 else 128 if N < 128 else 256
-        if policy == 0:
-            while G < 64 and B * G * 2 <= 64 * n_simd:
-                G *= 2
-        return G
-
-    for N in (1, 10, 15, 16, 20, 30, 31, 32, 50, 63, 64, 100, 127, 128, 255):
-        for B in (1, 64, 1024, 2048, 4096, 100000):
-            for pol in (0, 1):
-                assert bench.group_size(N, B, 1024, pol) == cpp_rule(N, B, 1024, pol)
-    assert bench.group_size(20, 1024, 1024) == 64 and bench.group_size(30, 4096, 1024) == 32
-    # kernels.h launch_solve_model: a 32-lane group widened to a wave runs replicated (unicycle)
-    assert bench.kernel_group("UnicycleFreeModel", 20, 1024, 1024) == (32, 2)
-    assert bench.kernel_group("UnicycleFreeModel", 20, 1024, 1024, 1) == (32, 1)
-    assert bench.kernel_group("UnicycleScanModel", 30, 1024, 1024) == (64, 1)
-    assert bench.kernel_group("LinearModel<5, 1>", 100, 2048, 1024) == (128, 1)
     old = os.environ.get("OMP_NUM_THREADS")
     os.environ["OMP_NUM_THREADS"] = "1"
     try:
@@ -226,7 +208,7 @@ def test_bench_solve_roofline_uses_only_a_current_pmc_record(tmp_path, monkeypat
         meta = {"mpcx_source_hash": _lib.source_hash() if current else "0000000000000000"}
         with open(tmp_path / bench.SOLVE_PMC, "w") as f:
             json.dump({"_meta": meta, **rec}, f)
-        r = bench.solve_roofline("UnicycleFreeModel", 32, algo, 100000, 2.0, R=2)  # 4e9 flops in 2 ms
+        r = bench.solve_roofline(kname, algo, 100000, 2.0)  # 4e9 flops in 2 ms
         assert r["achieved"] == pytest.approx(2.0) and r["frac"] == pytest.approx(2.0 / bench.PEAK_FP64_TFLOPS, abs=1e-5)
         if current:
             assert r["issued"]["algorithmic_over_issued"] == pytest.approx(0.1)
