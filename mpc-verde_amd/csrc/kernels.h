@@ -27,6 +27,7 @@
 #include <type_traits>
 
 #include "collectives.h"
+#include "fastmath.h"
 #include "models.h"
 #include "ode.h"
 #include "pscan.h"
@@ -133,7 +134,7 @@ __device__ __forceinline__ double barrier_logsum(const double* z, const BL& lb, 
     m *= hU[i] ? mu : 1.0;
     e += hU[i] ? eu : 0;
   }
-  return log(m) + (double)e * 0.69314718055994530942;
+  return log_fd(m) + (double)e * 0.69314718055994530942;
 }
 
 // IPOPT's filter (W&B 2006 §2.4, Filter::AddEntry) held in LDS by the lanes of a group: lane k
@@ -1745,7 +1746,8 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     bool sw_set = false;
     auto switching = [&]() __attribute__((always_inline)) {
       if (gd < 0) {
-        sw_a = exp(log(kDeltaSw) + kSTheta * log(thk) - kSPhi * log(-gd));
+        static_assert(kDeltaSw == 1.0, "log(delta) = 0");
+        sw_a = exp_fd(kSTheta * log_fd(thk) - kSPhi * log_fd(-gd));
         amin = kGammaAlpha * fmin(kGammaTheta, fmin(kGammaPhi * thk / (-gd), sw_a));
       }
       sw_set = true;

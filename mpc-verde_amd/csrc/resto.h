@@ -892,7 +892,7 @@ __device__ __forceinline__ void recover(RecIO& io, FilterLds<G>& filt, const Mod
     if (tiny < 10.0 * kEps) {
       accepted = ftype = tiny_flag = true;
     } else {
-      const double sw_a = gd < 0 ? exp(log(kDeltaSw) + kSTheta * log(thk) - kSPhi * log(-gd)) : 0.0;
+      const double sw_a = gd < 0 ? exp_fd(kSTheta * log_fd(thk) - kSPhi * log_fd(-gd)) : 0.0;  // kDeltaSw = 1
       const double amin = gd < 0 ? kGammaAlpha * fmin(kGammaTheta, fmin(kGammaPhi * thk / (-gd), sw_a))
                                  : kGammaAlpha * kGammaTheta;
       for (int ls = 0; ls < 80; ++ls) {

@@ -3,6 +3,7 @@
 // weighted-moment assembly the solve kernel uses) and uni_derivs<true> (the per-point formula)
 // at the same (x, u, x_ref, u_ref, lam, fs).  Built into tests/hip/libstage_check.so; used by
 // tests/test_gpu_stage.py only.
+#include "fastmath.h"
 #include "models.h"
 #include "riccati.h"
 #include "unicycle.h"
@@ -73,7 +74,21 @@ __global__ void riccati_check_kernel(int n, const double* in, double* out) {
   for (int j = 0; j < 2; ++j) o[16 + j] = kf[j];
 }
 
+// the kernel's fp64 log and exp (fastmath.h): out[2 i] = log_fd(x_i), out[2 i + 1] = exp_fd(y_i)
+__global__ void fastmath_check_kernel(int n, const double* x, const double* y, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[2 * i] = log_fd(x[i]);
+  out[2 * i + 1] = exp_fd(y[i]);
+}
+
 }  // namespace mpcx
+
+extern "C" int fastmath_check(int n, const double* x, const double* y, double* out) {
+  if (n <= 0) return -3;
+  hipLaunchKernelGGL(mpcx::fastmath_check_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, n, x, y, out);
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -2;
+}
 
 extern "C" int riccati_check(int n, const double* in, double* out) {
   if (n <= 0) return -3;
