@@ -123,14 +123,16 @@ __device__ __forceinline__ double greduce(double v, XWave<G>& xw) {
   }
   return v;
 }
-// Several group reductions at once (OPS: 0 sum, 1 max, 2 min, one per value): the in-wave DPP
-// chains as greduce's, and for groups wider than a wave ONE LDS exchange and barrier for all of
-// them (a barrier is the expensive part there: the waves of a group meet at every one).
+// Several group reductions at once (OPS: 0 sum, 1 max, 2 min, 3 "all" of 0/1 flags, one per
+// value): the in-wave DPP chains as greduce's -- for "all" one ballot when the group fills the
+// wave -- and for groups wider than a wave ONE LDS exchange and barrier for all of them (a barrier
+// is the expensive part there: the waves of a group meet at every one).
 __device__ __forceinline__ double op_apply(int op, double a, double b) {  // op a compile-time constant after unrolling
   return op == 0 ? a + b : op == 1 ? qmax(a, b) : qmin(a, b);
 }
 template <int G>
 __device__ __forceinline__ double wreduce(int op, double v) {  // over the group's lanes inside one wave
+  if (G >= 64 && op == 3) return __ballot(!(v > 0.5)) == 0 ? 1.0 : 0.0;  // every (active) lane holds 1
   v = op_apply(op, v, dpp<kQuadXor1>(v));
   v = op_apply(op, v, dpp<kQuadXor2>(v));
   v = op_apply(op, v, dpp<kHalfMirror>(v));
@@ -189,8 +191,10 @@ __device__ __forceinline__ double gmin(double v, XWave<G>& xw) {
 // the wave: G, or 64 for a replicated 32-lane group (kernels.h R = 2), whose test is wave-uniform.
 template <int G, int L = G>
 __device__ __forceinline__ bool gall(bool c, XWave<G>& xw) {
-  if constexpr (G > 64) {
-    return greduce<G, OpMin>(c ? 1.0 : 0.0, xw) > 0.5;
+  if constexpr (G > 64) {  // a ballot per wave, one exchange
+    double t = c ? 1.0 : 0.0;
+    greduce_n<G, 3>(&t, xw);
+    return t > 0.5;
   } else {
     const unsigned long long f = __ballot(!c);  // lanes where c fails
     if constexpr (L >= 64) {

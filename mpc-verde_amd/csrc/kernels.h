@@ -261,14 +261,6 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   __shared__ double sbuf[Model::kParallelRiccati ? RElem<NX>::NE * kSBS : 1];
   // LDS cache of the ODE models' transcendental values across their derivative passes (ode.h)
   __shared__ double tcache[Model::kTrigSlots > 0 ? Model::kTrigSlots * kSBS : 1];
-  // the unicycle's narrow 32-lane groups (models.h stage_derivs): the lower half of the
-  // evaluation's moment sums waits here while the upper half is summed, instead of in registers
-#ifdef MPCX_EXP_LO_LDS
-  constexpr bool kLoStash = ReplicateOf<Model>::value && G == 32 && R == 1;
-#else
-  constexpr bool kLoStash = false;
-#endif
-  __shared__ double lostash[kLoStash ? kUniMoments * kSBS : 1];
   // the decoupled suffix's vector scan (multi-wave groups): two NX-double buffers per thread, then
   // the matrix powers (A^T)^(j 4^l), j = 1..3, l < 5, kept for the launch (table index pow_tab)
   __shared__ double dscan[DecSuffixOf<Model>::value && G > 64 ? 2 * NX * kSBS + 15 * NX * NX : 1];
@@ -310,10 +302,6 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     ModelArgs m = model_args(a);
     if (Model::kTrigSlots > 0) {
       m.tc = tcache + threadIdx.x;
-      m.tc_stride = kSBS;
-    }
-    if (kLoStash) {
-      m.tc = lostash + threadIdx.x;
       m.tc_stride = kSBS;
     }
     return m;
@@ -376,7 +364,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   auto group_tests2 = [&](bool c0_, bool c1_, bool& r0, bool& r1) __attribute__((always_inline)) {
     if constexpr (G > 64) {
       double t[2] = {c0_ ? 1.0 : 0.0, c1_ ? 1.0 : 0.0};
-      greduce_n<G, 2, 2>(t, xw);
+      greduce_n<G, 3, 3>(t, xw);
       r0 = t[0] > 0.5;
       r1 = t[1] > 0.5;
     } else {
@@ -1462,10 +1450,11 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
       // Decoupled suffix of a multi-wave group (G > 64): the reused path sums the suffix's vector
       // part by the log-depth scan, the full recursion in chain order.  A fresh delta = 0
       // factorisation has just stored the suffix's P_k -- the bits the cross-launch cache would
-      // hold -- so it is redone on the reused path: an instance's result then does not depend on
-      // the cache state (a fresh handle, an earlier launch's cache, a step of a multi-step launch)
+      // hold -- so it is redone on the reused path (block-uniform; the scan's conditions): an
+      // instance's result then does not depend on the cache state (a fresh handle, an earlier
+      // launch's cache, a step of a multi-step launch, a device schedule that bypasses the cache)
       if constexpr (kDec && G > 64) {
-        if (need && ok && !pcv && delta == 0.0 && kb < N && pcache_ok(fs)) {  // block-uniform
+        if (need && ok && !pcv && delta == 0.0 && kb < N && !a.lin.per_instance && a.tabseq == nullptr) {
           pcv = true;
           continue;
         }
@@ -1706,7 +1695,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     // amax, az (min), gd (sum) and the tiny-step test (max over the group < 0) in one exchange
     double fr[4] = {amax_l, az_l, gd_l, tiny_l < 0.0 ? 1.0 : 0.0};
     if constexpr (G > 64) {
-      greduce_n<G, 2, 2, 0, 2>(fr, xw);
+      greduce_n<G, 2, 2, 0, 3>(fr, xw);
     } else {
       greduce_n<G, 2, 2, 0>(fr, xw);
       fr[3] = gall<G, G * R>(tiny_l < 0.0, xw) ? 1.0 : 0.0;
@@ -1757,14 +1746,75 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
     double Lt0 = 0.0;        // (kEvalInSearch) this lane's barrier log-sum at the first trial point
     bool acc0 = false;       // accepted at the first trial of the filter line search
     if constexpr (!Model::kSOC) {
-    for (int ls = 0; ls < 80; ++ls) {
-      if (!__any(searching)) break;
+    // one trial point: the barrier term, the group sums of theta and phi, the filter test and
+    // IPOPT's acceptance (sufficient decrease -- switching condition + Armijo, or theta/phi
+    // decrease -- then the filter: IPOPT's order, which decides whether a rejection was the filter's)
+    auto trial_accept = [&](int ls, double tht_l, double pht_l, const double* zt) __attribute__((always_inline)) {
+      const double Lt = barrier_logsum<NZ>(zt, lb, ub, hL, hU);
+      if (ls == 0) Lt0 = Lt;
+      pht_l -= mu * Lt;
+      double tp_[2] = {tht_l, pht_l};
+      greduce_n<G, 0, 0>(tp_, xw);
+      const double tht = tp_[0], pht = tp_[1];
+      const bool infilter = filt.contains(tht, pht, xw);
+      if (searching) {
+        bool acc = isfinite(pht) && isfinite(tht) && tht <= theta_max;
+        bool ft = false;
+        if (acc) {
+          const bool sw = gd < 0 && alpha > sw_a;
+          if (thk <= theta_min && sw) {
+            acc = pht - phk <= kEtaPhi * alpha * gd + 10.0 * kEps * fabs(phk);
+            ft = acc;
+          } else {
+            acc = tht <= (1.0 - kGammaTheta) * thk || pht <= phk - kGammaPhi * thk + 10.0 * kEps * fabs(phk);
+          }
+        }
+        if (acc && infilter) {
+          acc = false;
+          lastrej_f = true;
+        } else if (!acc) {
+          lastrej_f = false;
+        }
+        if (infilter) DIAG(6);
+        if (acc) {
+          searching = false;
+          accepted = true;
+          ftype = ft;
+          trial_fresh = Model::kEvalInSearch && ls == 0;
+          acc0 = ls == 0;
+          if (ft) DIAG(7);
+        } else {
+          DIAG(2);
+          alpha *= 0.5;
+          if (alpha < amin) searching = false;  // would need restoration
+        }
+      }
+    };
+    // a trial's constraint violation and objective by the value function (every lane: group_next)
+    auto trial_value_sums = [&](const double* zt, double& tht_l, double& pht_l) __attribute__((always_inline)) {
+      double xtn[NX];
+      group_next<G, NX>(zt, xtn, xw);
+      double xft[NX], qt, ze[NZ];
+      stage_point(zt, ze);
+      Model::value(ma, ctx, ze, xft, qt);
+      if (hasU) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) tht_l += fabs(xft[i] - xtn[i]);
+        pht_l = fs * qt;
+      }
+      if (valid && k == 0)
+#pragma unroll
+        for (int i = 0; i < NX; ++i) tht_l += fabs(x0[i] - zt[i]);
+    };
+    // the first trial (alpha = alpha_max) as straight-line code ahead of the backtracking loop:
+    // the usual iteration accepts it and runs no loop control
+    if (__any(searching)) {
       phase();
       double zt[NZ];
 #pragma unroll
       for (int i = 0; i < NZ; ++i) zt[i] = fma(alpha, dz[i], z[i]);  // the update's exact expression
       double tht_l = 0, pht_l = 0;
-      if (Model::kEvalInSearch && ls == 0) {
+      if constexpr (Model::kEvalInSearch) {
         if (searching) {  // group-uniform (block-uniform for multi-wave groups)
           double lt[NX];
 #pragma unroll
@@ -1783,61 +1833,20 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
           pht_l = fs * qv;  // masked to 0 without an interval
         }
       } else {
-        double xtn[NX];
-        group_next<G, NX>(zt, xtn, xw);
-        double xft[NX], qt, ze[NZ];
-        stage_point(zt, ze);
-        Model::value(ma, ctx, ze, xft, qt);
-        if (hasU) {
-#pragma unroll
-          for (int i = 0; i < NX; ++i) tht_l += fabs(xft[i] - xtn[i]);
-          pht_l = fs * qt;
-        }
-        if (valid && k == 0)
-#pragma unroll
-          for (int i = 0; i < NX; ++i) tht_l += fabs(x0[i] - zt[i]);
+        trial_value_sums(zt, tht_l, pht_l);
       }
-      const double Lt = barrier_logsum<NZ>(zt, lb, ub, hL, hU);
-      if (ls == 0) Lt0 = Lt;
-      pht_l -= mu * Lt;
-      double tp_[2] = {tht_l, pht_l};
-      greduce_n<G, 0, 0>(tp_, xw);
-      const double tht = tp_[0], pht = tp_[1];
-      const bool infilter = filt.contains(tht, pht, xw);
-      if (searching) {
-        // sufficient decrease (switching condition + Armijo, or theta/phi decrease), then the
-        // filter -- IPOPT's order, which decides whether a rejection was the filter's
-        bool acc = isfinite(pht) && isfinite(tht) && tht <= theta_max;
-        bool ft = false;
-        if (acc) {
-          const bool sw = gd < 0 && alpha > sw_a;
-          if (thk <= theta_min && sw) {
-            acc = pht - phk <= kEtaPhi * alpha * gd + 10.0 * kEps * fabs(phk);
-            ft = acc;
-          } else {
-            acc = tht <= (1.0 - kGammaTheta) * thk || pht <= phk - kGammaPhi * thk + 10.0 * kEps * fabs(phk);
-          }
-        }
-        if (acc && infilter) {
-          acc = false;
-          lastrej_f = true;
-        } else if (!acc) {
-          lastrej_f = false;
-        }
-        if (searching && infilter) DIAG(6);
-        if (acc) {
-          searching = false;
-          accepted = true;
-          ftype = ft;
-          trial_fresh = Model::kEvalInSearch && ls == 0;
-          acc0 = ls == 0;
-          if (ft) DIAG(7);
-        } else {
-          DIAG(2);
-          alpha *= 0.5;
-          if (alpha < amin) searching = false;  // would need restoration
-        }
-      }
+      trial_accept(0, tht_l, pht_l, zt);
+    }
+    // backtracking: the further trials evaluate values only
+    for (int ls = 1; ls < 80; ++ls) {
+      if (!__any(searching)) break;
+      phase();
+      double zt[NZ];
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) zt[i] = fma(alpha, dz[i], z[i]);
+      double tht_l = 0, pht_l = 0;
+      trial_value_sums(zt, tht_l, pht_l);
+      trial_accept(ls, tht_l, pht_l, zt);
     }
     if constexpr (kSoftInline) {
       // ---- IPOPT's soft restoration step (resto.h step 1), taken here, out of the hot path,

@@ -69,12 +69,12 @@ struct UnicycleModel {
   }
   // the same with the moments summed in the replicated groups' two halves: the 32-lane groups,
   // which a small batch runs replicated (stage_derivs below), so that a node's bits do not depend
-  // on the batch it is solved in (the lower half waits in the kernel's LDS column a.tc, if given)
+  // on the batch it is solved in
   __device__ __forceinline__ static void derivs_halves(const ModelArgs& a, const Ctx& c, const double* z,
                                                        const double* ln, double fs, double* xf, double& q, double* A,
                                                        double* Bm, double* g, double* H) {
     const double u2[2] = {z[3], z[4]};
-    uni_derivs_moments<1>(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H, 0, a.tc, a.tc_stride);
+    uni_derivs_moments<1>(a.sp, z, u2, c.xr, c.ur, ln, fs, xf, q, A, Bm, g, H);
   }
   // the same evaluation split between the two replicas of a replicated lane group (kernels.h R = 2;
   // every lane of the wave must call it)

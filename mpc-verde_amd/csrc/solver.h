@@ -91,7 +91,7 @@ struct ModelArgs {
   LinTables lin;
   OdeParams op;
   int p_layout, N;
-  double* tc = nullptr;  // this lane's slot 0 of an LDS column: the ODE models' value cache, the unicycle's moment stash
+  double* tc = nullptr;  // ODE models: this lane's slot 0 of the solve kernel's LDS value cache
   int tc_stride = 0;     // slot stride (threads per block)
 };
 __host__ __device__ inline ModelArgs model_args(const SolveArgs& a) { return ModelArgs{a.sp, a.lin, a.op, a.p_layout, a.N}; }

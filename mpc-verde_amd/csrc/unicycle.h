@@ -128,15 +128,11 @@ __device__ __forceinline__ void uni_value(const StageParams& sp, const double x[
 // RS = 1 (one lane per node, models that also run replicated): the same two half-sums on one lane,
 // so that a node's bits do not depend on whether its group was replicated.  RS = 0: one sequential
 // sum (models that never run replicated: the halves would only hold more registers).
-// With RS = 1 and lo != nullptr the lower half's sums wait in memory (lo[i * lo_stride], an LDS
-// column of kUniMoments doubles) while the upper half is summed: the same bits, fewer registers.
-constexpr int kUniMoments = 21;
 template <int RS = 1>
 __device__ __forceinline__ void uni_derivs_moments(const StageParams& sp, const double x[3], const double u[2],
                                                    const double xr[3], const double ur[2], const double lam[3],
                                                    double fs, double xf[3], double& q, double A[9], double Bm[6],
-                                                   double g[5], double H[15], int rho = 0, double* lo = nullptr,
-                                                   int lo_stride = 0) {
+                                                   double g[5], double H[15], int rho = 0) {
   static_assert(RS >= 0 && RS <= 2, "sequential, split on one lane, or two replicas");
   const double v = u[0], w = u[1], th = x[2];
   const double h = sp.h, hh = 0.5 * h, h6 = h / 6.0, h3 = h / 3.0, third = 1.0 / 3.0;
@@ -222,27 +218,13 @@ __device__ __forceinline__ void uni_derivs_moments(const StageParams& sp, const 
 #define MPCX_UNI_MOMENTS(X) \
   X(qs) X(Sa) X(Sb) X(Sa1) X(Sb1) X(Sa2) X(Sb2) X(Saa) X(Sbb) X(Sab) X(Saa1) X(Sbb1) X(Sab1) X(Sba1) X(Sa1a1) \
   X(Sb1b1) X(Saa2) X(Sbb2) X(W0) X(Wt) X(Wtt)
-    if (lo != nullptr) {
-      typedef __attribute__((address_space(3))) double lds_double;
-      lds_double* l3 = (lds_double*)lo;  // an LDS column: ds_write / ds_read, not flat accesses
-      int slot = 0;
-#define MPCX_LO_PUT(s) l3[(slot++) * lo_stride] = s; s = 0.0;
-#define MPCX_LO_GET(s) s = l3[(slot++) * lo_stride] + s;
-      MPCX_UNI_MOMENTS(MPCX_LO_PUT)
-      for (int m = M0; m < sp.M; ++m) substep(true);
-      slot = 0;
-      if (sp.cost == 0) { MPCX_UNI_MOMENTS(MPCX_LO_GET) }
-#undef MPCX_LO_GET
-#undef MPCX_LO_PUT
-    } else {
 #define MPCX_LO_TAKE(s) const double lo_##s = s; s = 0.0;
 #define MPCX_LO_ADD(s) s = lo_##s + s;
-      MPCX_UNI_MOMENTS(MPCX_LO_TAKE)
-      for (int m = M0; m < sp.M; ++m) substep(true);
-      if (sp.cost == 0) { MPCX_UNI_MOMENTS(MPCX_LO_ADD) }
+    MPCX_UNI_MOMENTS(MPCX_LO_TAKE)
+    for (int m = M0; m < sp.M; ++m) substep(true);
+    if (sp.cost == 0) { MPCX_UNI_MOMENTS(MPCX_LO_ADD) }
 #undef MPCX_LO_ADD
 #undef MPCX_LO_TAKE
-    }
 #undef MPCX_UNI_MOMENTS
   } else {
     const int M0 = sp.M / 2;  // replica 0: substeps [0, M0), replica 1: [M0, M)
