@@ -10,7 +10,7 @@
 // against the library on 10^6 arguments per decade, tests/test_gpu_stage.py).  Arguments outside
 // the reduced ranges (0, subnormal, inf, nan; |x| > 708 for exp) take the library routine.
 //
-// The C++ oracle (oracle/ipm_ref.cpp) keeps std::log / std::pow: the kernel's barrier terms already
+// The C++ CPU restatement (test infrastructure) keeps std::log / std::pow: the kernel's barrier terms already
 // differ from it at the ulp level (one log of a mantissa product per lane, kernels.h
 // barrier_logsum), and the iteration counts are compared against it (tests/test_gpu_parity.py).
 #pragma once
