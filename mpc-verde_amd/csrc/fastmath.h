@@ -7,8 +7,9 @@
 // single-precision-free argument reductions with a minimax polynomial (Sun's fdlibm e_log.c /
 // e_exp.c algorithms, restated; error below 1 ulp there), with the one division each takes
 // formed by v_rcp_f64 and two Newton steps: ~30 and ~25 instructions, error <= 2 ulp (measured
-// against the library on 10^6 arguments per decade, tests/test_gpu_stage.py).  Arguments outside
-// the reduced ranges (0, subnormal, inf, nan; |x| > 708 for exp) take the library routine.
+// against the library on 10^6 arguments over the whole range, tests/test_gpu_stage.py).  Special
+// arguments (0, inf, nan, under/overflow) are handled by selects and clamps, not by a fallback to
+// the library routine.
 //
 // The C++ CPU restatement (test infrastructure) keeps std::log / std::pow: the kernel's barrier terms already
 // differ from it at the ulp level (one log of a mantissa product per lane, kernels.h
@@ -22,9 +23,10 @@ namespace mpcx {
 
 constexpr double kLn2Hi = 6.93147180369123816490e-01, kLn2Lo = 1.90821492927058770002e-10;
 
-// log(x) for x > 0
-__device__ __forceinline__ double log_fd(double x) {
-  if (!(x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308)) return log(x);  // 0, subnormal, inf, nan
+// log(x) for a normal x > 0 (or nan: propagated); no library fallback, so no second code path
+// holds registers -- the barrier log-sums' arguments are products of at most 2 NZ frexp
+// mantissas, in [2^-16, 1]
+__device__ __forceinline__ double log_fd_normal(double x) {
   double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
   int k = __builtin_amdgcn_frexp_exp(x);
   if (m < 0.70710678118654752440) {  // m in [sqrt(1/2), sqrt(2))
@@ -42,9 +44,18 @@ __device__ __forceinline__ double log_fd(double x) {
   return dk * kLn2Hi - ((hfsq - fma(s, hfsq + R, dk * kLn2Lo)) - f);
 }
 
-// exp(x)
+// log(x) for any x >= 0 (or nan): the frexp reduction also normalises subnormals; 0 and inf by
+// selects -- no library fallback, whose second code path would hold registers where the kernel
+// calls this (measured: a guarded version cost config 2 several per cent)
+__device__ __forceinline__ double log_fd(double x) {
+  const double r = log_fd_normal(x);
+  return x == 0.0 ? -INFINITY : (x == INFINITY ? INFINITY : r);
+}
+
+// exp(x), any x: the argument is clamped to [-1100, 1100] (exp underflows to 0 / overflows to inf
+// there already; nan passes through), and ldexp rounds the subnormal range correctly
 __device__ __forceinline__ double exp_fd(double x) {
-  if (!(x > -708.0 && x < 709.0)) return exp(x);  // under/overflow, inf, nan
+  x = x < -1100.0 ? -1100.0 : (x > 1100.0 ? 1100.0 : x);
   const double kd = rint(x * 1.44269504088896338700);
   const double hi = fma(-kd, kLn2Hi, x), lo = kd * kLn2Lo;  // x - k ln2 (hi exact: |k| < 2^11)
   const double r = hi - lo, t = r * r;

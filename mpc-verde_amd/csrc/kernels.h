@@ -134,7 +134,7 @@ __device__ __forceinline__ double barrier_logsum(const double* z, const BL& lb, 
     m *= hU[i] ? mu : 1.0;
     e += hU[i] ? eu : 0;
   }
-  return log_fd(m) + (double)e * 0.69314718055994530942;
+  return log_fd_normal(m) + (double)e * 0.69314718055994530942;
 }
 
 // IPOPT's filter (W&B 2006 §2.4, Filter::AddEntry) held in LDS by the lanes of a group: lane k

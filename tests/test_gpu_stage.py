@@ -180,3 +180,4 @@ def test_fast_log_exp_accuracy(harness):
             ulp = np.abs(got[fin] - ref[fin]) / np.spacing(np.abs(ref[fin]))
             print(f"max {ulp.max():.2f} ulp over {fin.sum()} finite values")
             assert ulp.max() <= 2.0
+
