@@ -1,5 +1,7 @@
 set -o pipefail
-mkdir -p gpurun_out/r05f
-timeout -k 10 300 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_gpu_stage.py > gpurun_out/r05f/stage.log 2>&1; tail -2 gpurun_out/r05f/stage.log
-tools/ab.sh mpc-verde_amd/mpcx/libmpcx.so mpc-verde_amd/mpcx/libmpcx_tay.so "" 2
-tools/ab_tree.sh "" 2 ab_m2 . && mkdir -p gpurun_out/ab2 && cp gpurun_out/ab/*.json gpurun_out/ab2/ && tools/ab_tree.sh "--config 5" 2 ab_base0 ab_m2 .
+L=mpc-verde_amd/mpcx
+for i in 1 2; do for lib in libmpcx libmpcx_redo1 libmpcx_galld; do
+  MPCX_LIB=$L/$lib.so MPCX_ALLOW_STALE_LIB=1 timeout -k 10 200 python3 bench.py --config 5 --no-cpu --no-roofline --no-reference-warm-start > gpurun_out/ab5_${lib}_$i.json 2>/dev/null || exit 1
+  python3 -c "import json;d=json.loads([l for l in open('gpurun_out/ab5_${lib}_$i.json') if l.startswith('{')][-1]);print('$lib', d['value'], d['lockstep']['value'], d['solve_kernel']['us_per_ipm_iteration'], d['solve_kernel']['timed_launch_ms'])"
+done; done
+(cd ab_base0 && timeout -k 10 200 python3 bench.py --config 5 --no-cpu --no-roofline --no-reference-warm-start > ../gpurun_out/ab5_base0.json 2>/dev/null; python3 -c "import json;d=json.loads([l for l in open('../gpurun_out/ab5_base0.json') if l.startswith('{')][-1]);print('base0', d['value'], d['lockstep']['value'], d['solve_kernel']['us_per_ipm_iteration'], d['solve_kernel']['timed_launch_ms'])")

@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--N", type=int, default=20)
     ap.add_argument("--model", choices=("unicycle", "pend", "kin_bicycle", "dyn_bicycle", "cartpole"),
                     default="unicycle")
+    ap.add_argument("--run", type=int, default=0,
+                    help="stamp one K-step launch (DeviceLoop.run(K), the bench's timed path) instead of one solve; "
+                         "cycles per iteration are then per iteration of the slowest wave's K solves")
     a = ap.parse_args()
     lib = mpcx._lib.load()
     lib.mpcx_diag_set_stamp_buffer.argtypes = [ctypes.c_void_p]
@@ -72,10 +75,15 @@ def main():
     waves = (a.batch * G + 63) // 64
     buf = torch.zeros(waves * SLOTS, dtype=torch.int64, device="cuda")
     assert lib.mpcx_diag_set_stamp_buffer(ctypes.c_void_p(buf.data_ptr())) == 0
-    loop.solve()
-    torch.cuda.synchronize()
+    if a.run > 0:
+        _, it_k = loop.run(a.run)
+        torch.cuda.synchronize()
+        it_inst = it_k.cpu().numpy().sum(axis=0)
+    else:
+        loop.solve()
+        torch.cuda.synchronize()
+        it_inst = loop.iters.cpu().numpy()
     acc = buf.view(waves, SLOTS).cpu().numpy().astype(float)
-    it_inst = loop.iters.cpu().numpy()
     iters = np.array([it_inst[(w * 64) // G] if G >= 64 else it_inst[w * (64 // G):(w + 1) * (64 // G)].max()
                       for w in range(waves)])
     slow = int(np.argmax(acc.sum(axis=1)))
