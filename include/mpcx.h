@@ -127,7 +127,9 @@ typedef struct mpcx_spec {
      also selects the default.  mpcx_default_spec fills every field: the unicycle gets
      the reference script's acceptable_tol 1e-8 / acceptable_obj_change_tol 1e-6 (the problem of
      :181-197 as the script builds it), the ODE models IPOPT's defaults.  (mpcx.nlpsol without
-     options uses IPOPT's defaults for every model, as ca.nlpsol without options does.) */
+     options uses IPOPT's defaults for every model, as ca.nlpsol without options does.)
+     ABI change (round 4): acceptable_obj_change_tol = 0 used to be taken literally; it now
+     selects the default like every other 0 field (write 4.9e-324 for IPOPT's literal 0). */
   double dual_inf_tol, constr_viol_tol, compl_inf_tol;
   double acceptable_tol, acceptable_dual_inf_tol, acceptable_constr_viol_tol, acceptable_compl_inf_tol;
   double acceptable_obj_change_tol;

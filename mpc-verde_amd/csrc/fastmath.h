@@ -23,10 +23,9 @@ namespace mpcx {
 
 constexpr double kLn2Hi = 6.93147180369123816490e-01, kLn2Lo = 1.90821492927058770002e-10;
 
-// log(x) for a normal x > 0 (or nan: propagated); no library fallback, so no second code path
-// holds registers -- the barrier log-sums' arguments are products of at most 2 NZ frexp
-// mantissas, in [2^-16, 1]
-__device__ __forceinline__ double log_fd_normal(double x) {
+// log(x) for a finite x > 0 (subnormals included: frexp normalises them); no library fallback, so
+// no second code path holds registers
+__device__ __forceinline__ double log_fd_pos(double x) {
   double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
   int k = __builtin_amdgcn_frexp_exp(x);
   if (m < 0.70710678118654752440) {  // m in [sqrt(1/2), sqrt(2))
@@ -44,12 +43,14 @@ __device__ __forceinline__ double log_fd_normal(double x) {
   return dk * kLn2Hi - ((hfsq - fma(s, hfsq + R, dk * kLn2Lo)) - f);
 }
 
-// log(x) for any x >= 0 (or nan): the frexp reduction also normalises subnormals; 0 and inf by
-// selects -- no library fallback, whose second code path would hold registers where the kernel
-// calls this (measured: a guarded version cost config 2 several per cent)
+// log(x) for any x with IEEE's special values by selects: log(0) = -inf, log(inf) = inf, log(x < 0)
+// = log(nan) = nan -- no library fallback, whose second code path would hold registers where the
+// kernel calls this (measured: a guarded version cost config 2 several per cent).  The special
+// values matter: a line-search trial point whose slack rounds to exactly 0 (a bound of |b| = 200
+// at mu = 1e-9) must get phi = +inf and be rejected, not a finite barrier term.
 __device__ __forceinline__ double log_fd(double x) {
-  const double r = log_fd_normal(x);
-  return x == 0.0 ? -INFINITY : (x == INFINITY ? INFINITY : r);
+  const double r = log_fd_pos(x);
+  return x > 0.0 ? (x == INFINITY ? INFINITY : r) : (x == 0.0 ? -INFINITY : NAN);
 }
 
 // exp(x), any x: the argument is clamped to [-1100, 1100] (exp underflows to 0 / overflows to inf

@@ -134,7 +134,7 @@ __device__ __forceinline__ double barrier_logsum(const double* z, const BL& lb, 
     m *= hU[i] ? mu : 1.0;
     e += hU[i] ? eu : 0;
   }
-  return log_fd_normal(m) + (double)e * 0.69314718055994530942;
+  return log_fd(m) + (double)e * 0.69314718055994530942;  // m = 0 (a slack at its bound): -inf
 }
 
 // IPOPT's filter (W&B 2006 §2.4, Filter::AddEntry) held in LDS by the lanes of a group: lane k
@@ -386,6 +386,11 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   for (int i = 0; i < NX; ++i) xfree = xfree && !hL[i] && !hU[i];
   int kb = N + 1;
   bool pcv = false;
+  // the cross-launch cache was invalid at this solve's start (a cold handle, new tables): only
+  // such a solve publishes, so a launch that found a valid cache never rewrites its header while
+  // other groups may still be reading it (a group recovering from an inertia correction computes
+  // the suffix afresh but does not publish)
+  bool pc_miss = false;
   // the cross-launch cache of the suffix's P_k applies to shared tables at fs = 1 only
   auto pcache_ok = [&](double fs_) __attribute__((always_inline)) {
     return kDec && a.pcache != nullptr && fs_ == 1.0 && !a.lin.per_instance && a.tabseq == nullptr;
@@ -822,6 +827,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
         const bool d = !hasX || (xfree && (k == N || ctx.dec));
         kb = (int)gmax<G>(d ? -1.0 : (double)k, xw) + 1;
         pcv = false;
+        pc_miss = false;
         // the suffix's P_k as an earlier launch of these tables computed them at fs = 1 and
         // delta = 0 (from identical operands: the same bits this solve's first factorisation
         // would produce), so even the first factorisation takes the reused path
@@ -832,6 +838,8 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
 #pragma unroll
               for (int i = 0; i < NP; ++i) Pk[i] = a.pcache[(size_t)k * NP + i];
             pcv = true;
+          } else {
+            pc_miss = true;
           }
         }
       }
@@ -1486,7 +1494,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
       pcv = !failed && delta == 0.0;  // Pk now holds a delta = 0 factorisation
       // publish it for later launches (every writer stores the same bits; readers accept only
       // the header of an earlier launch, so a half-written cache is never read)
-      if (fresh_fac && pcv && pcache_ok(fs)) {
+      if (fresh_fac && pcv && pc_miss && pcache_ok(fs)) {
         if (k >= kb && k <= N)
 #pragma unroll
           for (int i = 0; i < NP; ++i) a.pcache[(size_t)k * NP + i] = Pk[i];

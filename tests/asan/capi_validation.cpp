@@ -88,6 +88,9 @@ int main() {
   EXPECT(mpcx_set_linear_tab_dev(nullptr, i32, 1) < 0);
   int32_t nw, ng, np;
   EXPECT(mpcx_dims(nullptr, &nw, &ng, &np) < 0);
+  int32_t lanes, reps;
+  char kname[256];
+  EXPECT(mpcx_launch_shape(nullptr, 16, &lanes, &reps, kname, (int32_t)sizeof(kname)) < 0);
   mpcx_destroy(nullptr);
 
   // a valid spec: created where a device exists, refused with a HIP error elsewhere
@@ -100,6 +103,10 @@ int main() {
     EXPECT(mpcx_solve_batch(h, 0, d, nullptr, nullptr, nullptr, nullptr, nullptr, d, nullptr, nullptr, nullptr,
                             nullptr, nullptr, nullptr) == 0);
     EXPECT(mpcx_set_linear_model(h, 1, d, d, d, d, i32, 1) < 0);  // not a linear handle
+    EXPECT(mpcx_launch_shape(h, 0, &lanes, &reps, kname, (int32_t)sizeof(kname)) < 0);
+    EXPECT(mpcx_launch_shape(h, 16, &lanes, &reps, kname, 8) < 0);  // name buffer too small
+    EXPECT(mpcx_launch_shape(h, 16, &lanes, &reps, kname, (int32_t)sizeof(kname)) == 0 && lanes >= 32 &&
+           std::strstr(kname, "solve_kernel<mpcx::UnicycleFreeModel") != nullptr);
     mpcx_destroy(h);
     std::printf("device present: handle created and destroyed\n");
   } else {

@@ -134,6 +134,23 @@ def test_config5_pendulum_qp_full_batch(mpcx):
     print(f"config 5 QP N=100 B=2048: max sampled input difference from the pinned QP oracle {worst:.2e}")
     assert worst <= U_TOL
     run_vs_lockstep(solver, P, K)
+    # a longer closed loop: the bench's warm-up steps and a 10-step launch, every solve status 0.  (A
+    # line-search trial whose slack rounds to exactly 0 at a bound of 200 -- mu = 1e-9, fraction to
+    # the boundary 1 - 1e-9 -- must get phi = +inf; a barrier log that returned a finite value for a
+    # zero slack once let instance 112 step onto its bound and fail the factorisation at step 12.)
+    import torch
+
+    from mpcx.device import DeviceLoop
+
+    loop = DeviceLoop(solver, P)
+    for _ in range(3):
+        loop.step()
+        torch.cuda.synchronize()
+        assert np.all(loop.status.cpu().numpy() == 0)
+    st, _ = loop.run(10)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert np.all(st == 0), np.argwhere(st != 0)[:10]
 
 
 def test_config5_swingup_full_batch(mpcx, C):

@@ -162,9 +162,10 @@ def test_fast_log_exp_accuracy(harness):
 
     rng = np.random.default_rng(3)
     x = np.concatenate([np.exp(rng.uniform(-708, 709, 2_000_000)), 1.0 + rng.uniform(-0.3, 0.3, 500_000),
-                        rng.uniform(0.5, 1.0, 500_000), [1.0, 0.5, 2.0, 1e-310, 0.0, np.inf, 2.2250738585072014e-308]])
+                        rng.uniform(0.5, 1.0, 500_000),
+                        [1.0, 0.5, 2.0, 1e-310, 0.0, np.inf, 2.2250738585072014e-308, -1.0, np.nan]])
     y = np.concatenate([rng.uniform(-745, 709, 2_000_000), rng.uniform(-1, 1, 1_000_000),
-                        [0.0, -800.0, 800.0, -np.inf, np.inf, 1e-300, -708.5]])
+                        [0.0, -800.0, 800.0, -np.inf, np.inf, 1e-300, -708.5, 5.0, np.nan]])
     n = x.size
     assert y.size == n
     harness.fastmath_check.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -175,7 +176,7 @@ def test_fast_log_exp_accuracy(harness):
     o = out.cpu().numpy().reshape(n, 2)
     with np.errstate(divide="ignore", over="ignore", under="ignore", invalid="ignore"):
         for got, ref in ((o[:, 0], np.log(x)), (o[:, 1], np.exp(y))):
-            fin = np.isfinite(ref) & (ref != 0)
+            fin = np.isfinite(ref) & (ref != 0)  # the special values: 0 -> -inf, inf, x < 0 and nan -> nan
             np.testing.assert_array_equal(got[~fin], ref[~fin])
             ulp = np.abs(got[fin] - ref[fin]) / np.spacing(np.abs(ref[fin]))
             print(f"max {ulp.max():.2f} ulp over {fin.sum()} finite values")
