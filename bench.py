@@ -46,7 +46,7 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # FP64 vector (VALU) peak: AMD's MI355X spec, half the FP32 vector peak of 157.3 TF/s
 # (MI355X_MICROARCH.md); the solve kernel issues scalar-per-lane FP64 FMAs, no MFMA
 PEAK_FP64_TFLOPS = 78.6
-SOLVE_PMC = os.path.join("profiles", "r04_solve_kernel_pmc.json")
+SOLVE_PMC = os.path.join("profiles", "r05_solve_kernel_pmc.json")
 SWEEP_BYTES_PER_STAGE = 256  # read x_k,u_k,x_{k+1} (64 B) + write c,q,A,B,grad q (192 B)
 SWEEP_BYTES_PER_INSTANCE = 48  # P
 
@@ -252,7 +252,7 @@ def usable_cpus():
 # recomputation on every lane, padding lanes and the line search's further trials are not
 # algorithmic work and are not counted).  Linear models' E is counted analytically (their
 # Jacobians and Hessians are tables).
-FLOP_PROBE = os.path.join("profiles", "r04_flop_probe.json")
+FLOP_PROBE = os.path.join("profiles", "r05_flop_probe.json")
 ALGO_KEYS = {  # workload -> (eval key or None for a linear model, riccati key)
     2: ("unicycle_quadrature_M4", "unicycle"), 3: ("unicycle_node_M1", "unicycle"),
     4: (None, "linear4x1"), 5: (None, "linear5x1"),

@@ -15,6 +15,8 @@
 #            the trial evaluation; libmpcx_sub5.so: config 5 with sub-phases; build them with
 #            `make -C mpc-verde_amd stamps` and tools/exp_build.sh, see tools/stamp_profile.py)
 #                                                                   -> gpurun_out/stamps_c2_sub.json, stamps_c5_sub.json
+#   flops    FP64 flops per unit of the building blocks (tools/flop_probe.py under --pmc)
+#                                                                   -> gpurun_out/flop_probe.json
 # A/B comparisons of source trees are tools/ab_tree.sh (trees from tools/base_build.sh).
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -53,6 +55,11 @@ for STEP in "$@"; do
       (cd "$R" && MPCX_STAMPS_LIB=$L/libmpcx_sub5.so MPCX_ALLOW_STALE_LIB=1 timeout -k 10 300 \
         python3 tools/stamp_profile.py --model pend --N 100 --batch 2048 --steps 3 > "$OUT/stamps_c5_sub.json" \
         2> "$OUT/stamps_c5_sub.err") ;;
+    flops)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 \
+        SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 --output-format csv -d "$OUT/flops" -o flops -- \
+        python3 "$R/tools/flop_probe.py" > "$OUT/flops.log" 2>&1)
+      python3 "$R/tools/flop_summary.py" "$OUT/flops" > "$OUT/flop_probe.json" ;;
     *)
       echo "unknown step $STEP" >&2; exit 2 ;;
   esac
