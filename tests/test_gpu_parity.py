@@ -267,6 +267,65 @@ def test_interval0_integrates_from_parameter(mpcx, R, C):
     assert np.max(np.abs(ref["lam_g"][:, 0:3])) <= 1e-8
 
 
+def _interval0_case(mpcx, name):
+    """(ocp, P, nx) of one non-config-2 kernel path for the interval-0 test below."""
+    from mpcx import dist as mdist
+    from mpcx import lti
+
+    if name == "c3_unicycle_scan":  # UnicycleScanModel (Riccati scan from N = 25), state bounds
+        _, P = mdist.config3_inputs(0, 256, N=30)
+        return mpcx.unicycle_tracking(N=30), P, 3
+    if name == "kin_bicycle_scan":  # OdeModel<KinBicycle>, Riccati scan
+        _, P = mdist.config3_bicycle_inputs(0, 256, N=30)
+        return mpcx.kinematic_bicycle_tracking(N=30), P, 3
+    if name == "swingup_two_waves":  # OdeModel<CartPole>, N = 100: two-wave groups (G = 128)
+        return mpcx.cartpole_swingup(N=100), mdist.config5_swingup_inputs(0, 128), 4
+    if name == "linear4_scan":  # LinearModel<4,1> (kScan: table Jacobians, Riccati scan), config 4's tables
+        t0, x0, par = mdist.config4_inputs(0, 256, N=50)
+        _, _, vref = mdist.lane_change()
+        ocp = mpcx.lateral_ltv(N=50, Delta=0.05, vref=vref, per_instance_tab=np.minimum(t0, 499))
+        return ocp, ocp.params(x0, par[np.minimum(t0, 499)]), 4
+    if name == "pendulum_qp_two_waves":  # LinearModel<5,1>, G = 128, decoupled suffix
+        lin = lti.inverted_pendulum_qp(N=100)
+        return lin, lti.pendulum_params(lin, mdist.config5_inputs(0, 256), 0.0), 5
+    raise ValueError(name)
+
+
+@pytest.mark.parametrize("name", ["c3_unicycle_scan", "kin_bicycle_scan", "swingup_two_waves", "linear4_scan",
+                                  "pendulum_qp_two_waves"])
+def test_interval0_from_parameter_other_paths(mpcx, C, name):
+    """The interval-0 formulation (X_0 enters only g_0 = x0 - X_0) on the kernel paths the
+    config-2 test above does not take: the Riccati scans (unicycle N = 30, kinematic bicycle,
+    LinearModel<4,1>), the two-wave groups of N = 100 (swing-up ODE, cart-pole QP with the
+    decoupled suffix).  From guesses whose X_0 is moved off x0 by up to 0.5: every status <= 1,
+    lam_g[0:nx] = 0 to the dual tolerance; the ODE/unicycle paths take the C++ oracle's iteration
+    counts from the same guesses and reach its optima; the QPs reach the cold solve's (unique) optimum."""
+    ocp, P, nx = _interval0_case(mpcx, name)
+    B = P.shape[0]
+    solver = mpcx.nlpsol("s", "mi355x", ocp, {"ipopt": {"max_iter": 3000}})
+    cold = solver.solve_batch(P)
+    assert np.all(cold["status"] <= 1), np.unique(cold["status"], return_counts=True)
+    w0 = cold["w"].copy()
+    w0[:, 0:nx] += np.random.default_rng(5).uniform(-0.5, 0.5, (B, nx))
+    r = solver.solve_batch(P, w0=w0)
+    assert np.all(r["status"] <= 1), np.unique(r["status"], return_counts=True)
+    lam0 = float(np.max(np.abs(r["lam_g"][:, 0:nx])))
+    print(f"{name}: max |lam_g[0:{nx}]| = {lam0:.1e}")
+    assert lam0 <= 1e-8
+    if name.startswith(("linear", "pendulum")):
+        errs = np.array([rel_err(r["w"][b], cold["w"][b]) for b in range(B)])
+        assert errs.max() <= 1e-6, errs.max()
+        return
+    ref = C.solve(ocp, P, w0=w0, nthreads=0, max_iter=3000)
+    assert np.all(ref["status"] <= 1)
+    n_it = int(np.sum(ref["iters"] != r["iters"]))
+    errs = np.array([rel_err(r["w"][b], ref["w"][b]) for b in range(B)])
+    print(f"{name}: {n_it} of {B} iteration counts differ from the C++ oracle (X_0 != x0 guesses), "
+          f"max optimum difference {errs.max():.1e}")
+    assert n_it == 0, np.flatnonzero(ref["iters"] != r["iters"])
+    assert errs.max() <= 1e-6, errs.max()
+
+
 # ----------------------------------------------------------------------------- edge cases
 @pytest.mark.parametrize("B", [1, 2, 3, 31, 33, 65])
 def test_ragged_batch_sizes(mpcx, R, B):
