@@ -112,6 +112,27 @@ def test_to_spec_mirrors_reference_constants():
     assert (t.lbx[0], t.ubx[0], t.lbx[1], t.ubx[1]) == (-20.0, 20.0, -2.0, 2.0)
 
 
+def test_to_spec_ipopt_option_mappings():
+    """The spec reads a 0 field as IPOPT's default (include/mpcx.h, capi.cpp solve args), so the
+    Python side maps IPOPT's literal values onto the spec: acceptable_obj_change_tol = 0 (the
+    objective must not change at all) -> 5e-324, acceptable_iter = 0 (heuristic off) -> -1;
+    left out, every option carries IPOPT's default explicitly."""
+    import mpcx
+    from mpcx.ocp import IPOPT_DEFAULTS
+
+    ocp = mpcx.unicycle_point_to_point(N=20)
+    s = mpcx.to_spec(ocp)
+    for k, v in IPOPT_DEFAULTS.items():
+        assert getattr(s, k) == v, k
+    z = mpcx.to_spec(ocp, ipopt={"acceptable_obj_change_tol": 0.0, "acceptable_iter": 0})
+    assert z.acceptable_obj_change_tol == 5e-324 and z.acceptable_obj_change_tol > 0.0
+    assert z.acceptable_iter == -1
+    r = mpcx.to_spec(ocp, ipopt={"acceptable_tol": 1e-8, "acceptable_obj_change_tol": 1e-6})
+    assert (r.acceptable_tol, r.acceptable_obj_change_tol) == (1e-8, 1e-6)
+    with pytest.raises(ValueError):
+        mpcx.to_spec(ocp, ipopt={"no_such_option": 1.0})
+
+
 def test_vec_coercion():
     from mpcx.nlpsol import _vec
 
