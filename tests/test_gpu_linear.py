@@ -506,6 +506,61 @@ def test_pendulum_suffix_cache_off_with_device_schedule(mpcx):
     mpcx._lib.check(lib.mpcx_set_linear_tab_dev(S._h.ptr, None, 0))
 
 
+def test_pendulum_run_with_schedule_changes_equals_lockstep(mpcx):
+    """Config 5 (N = 100, two-wave groups, the reused suffix as a radix-4 scan whose matrix
+    powers are formed once per launch): a multi-step run() whose schedules change from one
+    closed-loop step to the next (tabseq; per instance, the blocked stages alternate between
+    two tables with other weights) equals lock-step launches with the same schedules, bit for
+    bit -- the powers and the suffix formed for one step's tables are not reused for another's."""
+    import torch
+
+    from mpcx import lti
+    from mpcx.device import DeviceLoop
+
+    N, B, K = 100, 64, 4
+    rng = np.random.default_rng(9)
+    x = rng.uniform([-1, -.5, -.2, -.5], [1, .5, .2, .5], size=(B, 4))
+    l1 = lti.inverted_pendulum_qp(N=N)
+    l2 = lti.inverted_pendulum_qp(N=N, q=(1.5, 2.0))
+    A = np.concatenate([l1.A, l2.A[1:]])
+    Bm = np.concatenate([l1.B, l2.B[1:]])
+    W = np.concatenate([l1.W, l2.W[1:]])
+    sched = [np.array([0] * 5 + [1 + s] * (N - 5), np.int32) for s in (0, 1)]
+    lin = lti.LinearOCP(N=N, A=A, B=Bm, W=W, tab=sched[0], T=l1.T, u_lb=l1.u_lb, u_ub=l1.u_ub)
+    lin.x_target = l1.x_target
+    P = lti.pendulum_params(lin, x, 0.0)
+    S = mpcx.nlpsol("ts", "mi355x", lin, {"ipopt": {"max_iter": 200}})
+    tabs = np.stack([np.stack([sched[(t + b // 8) % 2] for b in range(B)]) for t in range(K)])
+    dt = torch.from_numpy(np.ascontiguousarray(tabs)).cuda()
+    lock = DeviceLoop(S, P)
+    st_l, it_l = [], []
+    for t in range(K):
+        lock.set_schedule(dt[t])
+        lock.step()
+        torch.cuda.synchronize()
+        st_l.append(lock.status.cpu().numpy().copy())
+        it_l.append(lock.iters.cpu().numpy().copy())
+    lock.set_schedule(None)
+    run = DeviceLoop(S, P)
+    run.set_schedule(dt[0])
+    st_r, it_r = run.run(K, tabseq=dt)
+    torch.cuda.synchronize()
+    run.set_schedule(None)
+    assert np.all(np.array(st_l) == 0)
+    np.testing.assert_array_equal(st_r.cpu().numpy(), np.array(st_l))
+    np.testing.assert_array_equal(it_r.cpu().numpy(), np.array(it_l))
+    for n in ("P", "w", "w0", "lam", "lamx", "f"):
+        got, want = getattr(run, n).cpu().numpy(), getattr(lock, n).cpu().numpy()
+        np.testing.assert_array_equal(got, want, err_msg=n)
+    # the schedules matter: one table throughout gives other inputs
+    one = DeviceLoop(S, P)
+    one.set_schedule(dt[0])
+    one.run(K, tabseq=dt[:1].expand(K, B, N).contiguous())
+    torch.cuda.synchronize()
+    one.set_schedule(None)
+    assert np.max(np.abs(one.w.cpu().numpy() - run.w.cpu().numpy())) > 1e-6
+
+
 def test_padded_double_integrator_closed_loop(mpcx, R):
     """A 2-state model (double integrator, no kernel instantiation of its own) through the
     CasADi-shaped call and the integrator, in the reference's closed-loop pattern
