@@ -47,6 +47,7 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # (MI355X_MICROARCH.md); the solve kernel issues scalar-per-lane FP64 FMAs, no MFMA
 PEAK_FP64_TFLOPS = 78.6
 SOLVE_PMC = os.path.join("profiles", "r05_solve_kernel_pmc.json")
+SOLVE_TRAFFIC = "r05_solve_traffic.json"  # HBM bytes of the timed launch (tools/solve_traffic.py)
 SWEEP_BYTES_PER_STAGE = 256  # read x_k,u_k,x_{k+1} (64 B) + write c,q,A,B,grad q (192 B)
 SWEEP_BYTES_PER_INSTANCE = 48  # P
 
@@ -124,6 +125,9 @@ def parse():
                     help="skip the second timing under the reference's warm start (shifted primal only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum timed CPU-baseline solve time")
     ap.add_argument("--profile-sweep-only", action="store_true", help="only launch the sweep (for rocprofv3 --pmc)")
+    ap.add_argument("--profile-solve-only", action="store_true",
+                    help="only the warm-up steps and the timed K-step launch, then exit (for rocprofv3 --pmc: "
+                         "tools/solve_traffic.py takes that launch's HBM bytes)")
     return ap.parse_args()
 
 
@@ -339,6 +343,11 @@ def solve_roofline(kernel, algo, group_iters, ms):
          "algorithmic_flops_per_launch": fl,
          "note": "the kernel is bound by the issue of each instance's serial chains (one wave per SIMD), "
                  "not by HBM (traffic = its inputs/outputs, see solve_kernel.hbm_frac) nor by FP64 throughput"}
+    tr, why_tr = load_solve_traffic(kernel)
+    if tr is not None:
+        r["traffic"] = tr
+    else:
+        r["traffic_note"] = why_tr
     pmc, why = load_solve_pmc(kernel)
     if pmc is None:
         r["issued"] = why
@@ -395,6 +404,25 @@ def sweep_roofline(solver, torch, B, N, reps, stream):
     del X, U, XR, J
     torch.cuda.empty_cache()
     return ms
+
+
+def load_solve_traffic(kernel):
+    """HBM bytes of the timed K-step solve launch from the committed PMC passes
+    (profiles/*_solve_traffic.json, tools/solve_traffic.py), when they measured the tree's
+    current sources and this kernel; else (None, why)."""
+    from mpcx import _lib
+
+    path = os.path.join(ROOT, "profiles", SOLVE_TRAFFIC)
+    if not os.path.exists(path):
+        return None, f"no {SOLVE_TRAFFIC}"
+    with open(path) as f:
+        d = json.load(f)
+    src = _lib.source_hash()
+    if d.get("mpcx_source_hash") != src:
+        return None, f"{SOLVE_TRAFFIC} measured sources {d.get('mpcx_source_hash')}, tree {src}"
+    if d.get("kernel") != kernel:
+        return None, f"{SOLVE_TRAFFIC} measured {d.get('kernel')}"
+    return float(d["hbm_bytes_per_launch"]), None
 
 
 def load_traffic(B, N):
@@ -578,6 +606,10 @@ def main():
                 loop.step(status_out=status_hist[i], iters_out=iters_hist[i])
         torch.cuda.synchronize()
         t1 = time.perf_counter()
+        if args.profile_solve_only:  # the timed launch is the last solve dispatch of this process
+            print(json.dumps({"profile_solve_only": True, "run_ms": ev_run[0].elapsed_time(ev_run[1])
+                              if args.mode == "async" else None, "solve_kernel": solver._h.launch_shape(B)[2]}))
+            sys.exit(0)
         if world > 1:
             torch.distributed.barrier()
         elapsed = mdist.max_over_ranks(t1 - t0, device=loop.P.device)

@@ -236,3 +236,12 @@ def test_bench_solve_roofline_uses_only_a_current_pmc_record(tmp_path, monkeypat
             assert r["issue"]["issuing_share_of_wave_cycles"] == 0.8
         else:
             assert isinstance(r["issued"], str) and r["issued"].startswith("stale") and "issue" not in r
+    # roofline.traffic: the counter-measured HBM bytes of the timed launch, only from a record of
+    # this tree's sources and this kernel (tools/solve_traffic.py)
+    for src, kern, want in ((_lib.source_hash(), kname, 7.5e6), ("0000000000000000", kname, None),
+                            (_lib.source_hash(), "other", None)):
+        with open(tmp_path / "profiles" / bench.SOLVE_TRAFFIC, "w") as f:
+            json.dump({"kernel": kern, "hbm_bytes_per_launch": 7.5e6, "mpcx_source_hash": src}, f)
+        r = bench.solve_roofline(kname, algo, 100000, 2.0)
+        assert r["traffic"] == want
+        assert (want is None) == ("traffic_note" in r)

@@ -15,6 +15,7 @@
 #            the trial evaluation; libmpcx_sub5.so: config 5 with sub-phases; build them with
 #            `make -C mpc-verde_amd stamps` and tools/exp_build.sh, see tools/stamp_profile.py)
 #                                                                   -> gpurun_out/stamps_c2_sub.json, stamps_c5_sub.json
+#   traffic  FETCH_SIZE / WRITE_SIZE passes of the bench's timed solve launch -> gpurun_out/solve_traffic.json
 #   flops    FP64 flops per unit of the building blocks (tools/flop_probe.py under --pmc)
 #                                                                   -> gpurun_out/flop_probe.json
 # A/B comparisons of source trees are tools/ab_tree.sh (trees from tools/base_build.sh).
@@ -55,6 +56,13 @@ for STEP in "$@"; do
       (cd "$R" && MPCX_STAMPS_LIB=$L/libmpcx_sub5.so MPCX_ALLOW_STALE_LIB=1 timeout -k 10 300 \
         python3 tools/stamp_profile.py --model pend --N 100 --batch 2048 --steps 3 > "$OUT/stamps_c5_sub.json" \
         2> "$OUT/stamps_c5_sub.err") ;;
+    traffic)
+      (cd /tmp && export TMPDIR=/tmp &&
+        timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/solve_fetch" -o pmc -- \
+          python3 "$R/bench.py" --profile-solve-only --no-cpu --no-roofline > "$OUT/solve_fetch.log" 2>&1 &&
+        timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/solve_write" -o pmc -- \
+          python3 "$R/bench.py" --profile-solve-only --no-cpu --no-roofline > "$OUT/solve_write.log" 2>&1)
+      python3 "$R/tools/solve_traffic.py" "$OUT/solve_fetch" "$OUT/solve_write" "$OUT/solve_traffic.json" ;;
     flops)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 \
         SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 --output-format csv -d "$OUT/flops" -o flops -- \
