@@ -9,6 +9,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 namespace mpcx {
 
 // v_mov_b32_dpp with bound_ctrl: lanes whose source is out of range read 0, so the
@@ -257,6 +259,33 @@ __device__ __forceinline__ void group_next(const double* v, double* out, XWave<G
       for (int i = 0; i < n; ++i) out[i] = b[wv * kXchStride + i];
     xw.slot ^= 1;
   }
+}
+
+// acc += (element E of a block-uniform matrix) * w, where lane r of every 16-lane row holds
+// element r of the matrix (m): v_fmac_f64 with a DPP row_newbcast source (gfx950's 64-bit DPP),
+// one instruction, no LDS round trip per element.  The s_nop covers the VALU-write -> DPP-read
+// hazard of m, which the compiler does not see inside the asm.
+template <int E>
+__device__ __forceinline__ void fmac_row_bcast(double& acc, double m, double w) {
+  static_assert(E >= 0 && E < 16, "row lane");
+  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(acc)
+               : "v"(m), "v"(w), "n"(E));
+}
+// acc[i] += sum_j M[i][j] w[j] (j ascending: the fma order of a plain loop) for an NX x NX matrix
+// held as mA = M[r], mB = M[16 + r] on row lane r (NX <= 5)
+template <int NX, int E>
+__device__ __forceinline__ void matvec_bcast_e(double* acc, const double* w, double mA, double mB) {
+  if constexpr (E < 16)
+    fmac_row_bcast<E>(acc[E / NX], mA, w[E % NX]);
+  else
+    fmac_row_bcast<E - 16>(acc[E / NX], mB, w[E % NX]);
+}
+template <int NX, int... E>
+__device__ __forceinline__ void matvec_bcast(double* acc, const double* w, double mA, double mB,
+                                             std::integer_sequence<int, E...>) {
+  static_assert(NX * NX <= 32, "two row registers");
+  (matvec_bcast_e<NX, E>(acc, w, mA, mB), ...);
 }
 
 // 1/x to full fp64 accuracy: v_rcp_f64 + two Newton steps (no IEEE division sequence

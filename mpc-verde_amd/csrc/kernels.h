@@ -1277,19 +1277,26 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
                 double* nxt = dscan + ((l + 1) & 1) * NX * kSBS;
 #pragma unroll
                 for (int q = 1; q <= 3; ++q) {
-                  if (t + q * d < G) {
-                    const double* M = mpow + (3 * l + q - 1) * NX * NX;
-                    double w[NX];
+                  // the matrix spread over each 16-lane row (lane r: elements r and 16 + r) and
+                  // applied by row-broadcast FMAs (collectives.h matvec_bcast): the block-uniform
+                  // elements were 25 broadcast LDS reads, each a round trip on the FMA chain.  Every
+                  // lane takes part (a broadcast source lane must be active); lanes without a
+                  // partner keep v.
+                  const double* M = mpow + (3 * l + q - 1) * NX * NX;
+                  const int r = t & 15;
+                  const double mA = M[r];
+                  const double mB = NX * NX > 16 ? M[16 + min(r, NX * NX - 17)] : 0.0;
+                  const bool on = t + q * d < G;
+                  const int src = on ? t + q * d : t;
+                  double w[NX], acc[NX];
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) w[i] = cur[i * kSBS + t + q * d];
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) {
-                      double acc = v[i];
-#pragma unroll
-                      for (int j = 0; j < NX; ++j) acc = fma(M[i * NX + j], w[j], acc);
-                      v[i] = acc;
-                    }
+                  for (int i = 0; i < NX; ++i) {
+                    w[i] = cur[i * kSBS + src];
+                    acc[i] = v[i];
                   }
+                  matvec_bcast<NX>(acc, w, mA, mB, std::make_integer_sequence<int, NX * NX>{});
+#pragma unroll
+                  for (int i = 0; i < NX; ++i) v[i] = on ? acc[i] : v[i];
                 }
 #pragma unroll
                 for (int i = 0; i < NX; ++i) nxt[i * kSBS + t] = v[i];

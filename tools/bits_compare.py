@@ -3,7 +3,7 @@
 that must not change any result): a cold solve_batch of a bench workload's batch and a 3-step
 device closed loop, saved to an .npz.
 
-    MPCX_LIB=... MPCX_ALLOW_STALE_LIB=1 python tools/bits_compare.py dyn OUT.npz
+    MPCX_LIB=... MPCX_ALLOW_STALE_LIB=1 python tools/bits_compare.py {c2,c5,dyn} OUT.npz
     python tools/bits_compare.py --diff A.npz B.npz
 """
 import os
@@ -36,6 +36,11 @@ if work == "dyn":  # config 4 variant: 6-state dynamic bicycle, N = 50, B = 1024
 elif work == "c2":  # config 2
     ocp = mpcx.unicycle_point_to_point(N=20)
     P = mdist.config2_inputs(0, 1024)
+elif work == "c5":  # config 5: cart-pole QP, N = 100, B = 2048 (two-wave groups, the suffix scan)
+    from mpcx import lti
+
+    ocp = lti.inverted_pendulum_qp(N=100)
+    P = lti.pendulum_params(ocp, mdist.config5_inputs(0, 2048), 0.0)
 else:
     raise SystemExit(f"unknown workload {work}")
 solver = mpcx.nlpsol("s", "mi355x", ocp, {"ipopt": {"max_iter": 3000}})
