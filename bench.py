@@ -608,7 +608,8 @@ def main():
         t1 = time.perf_counter()
         if args.profile_solve_only:  # the timed launch is the last solve dispatch of this process
             print(json.dumps({"profile_solve_only": True, "run_ms": ev_run[0].elapsed_time(ev_run[1])
-                              if args.mode == "async" else None, "solve_kernel": solver._h.launch_shape(B)[2]}))
+                              if args.mode == "async" else None, "solve_kernel": solver._h.launch_shape(B)[2],
+                              "mpcx_source_hash": _lib.source_hash()}))
             sys.exit(0)
         if world > 1:
             torch.distributed.barrier()

@@ -575,7 +575,10 @@ int mpcx_launch_shape(const mpcx_handle* h, int32_t B, int32_t* lanes, int32_t* 
 static int solve_launch(mpcx_handle* h, mpcx::SolveArgs& a, hipStream_t stream) {
   const int slots = mpcx::resto_ws_slots(a.model, a.nx, a.nu);
   if (slots > 0) {  // (the 6-state bicycle's chain stash needs it with restoration off too)
-    const int G = mpcx::solve_group_size(a.N, a.B, a.n_simd, a.group_policy);
+    int Gk = 0, R = 0;  // the launch's lanes per instance (the kernel's grid, kernels.h solve_shape)
+    const char* kname = nullptr;
+    if (mpcx::solve_shape(a, &Gk, &R, &kname) != hipSuccess) return fail(MPCX_EINVAL, "no kernel for this model");
+    const int G = Gk * R;
     const long bs = G > 64 ? G : 64;
     const long threads = ((long)a.B * G + bs - 1) / bs * bs;
     const size_t need = (size_t)slots * threads + 1;  // + the park flag

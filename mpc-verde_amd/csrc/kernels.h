@@ -1284,7 +1284,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
                   // partner keep v.
                   const double* M = mpow + (3 * l + q - 1) * NX * NX;
                   const int r = t & 15;
-                  const double mA = M[r];
+                  const double mA = M[min(r, NX * NX - 1)];  // (in bounds for NX * NX < 16 too)
                   const double mB = NX * NX > 16 ? M[16 + min(r, NX * NX - 17)] : 0.0;
                   const bool on = t + q * d < G;
                   const int src = on ? t + q * d : t;
@@ -2562,11 +2562,17 @@ template <class Model>
 static void solve_shape(const SolveArgs& a, int* G, int* R) {
   *G = solve_group_size(a.N, a.B, a.n_simd, a.group_policy);
   *R = 1;
-  if constexpr (ReplicateOf<Model>::value)
-    if (*G == 64 && solve_group_size(a.N, a.B, a.n_simd, 1) == 32) {
+  if constexpr (ReplicateOf<Model>::value) {
+    const int narrow = solve_group_size(a.N, a.B, a.n_simd, 1);
+    if (*G == 64 && narrow == 32) {
       *G = 32;
       *R = 2;
     }
+    // a replicating model's 32-lane kernel sums the evaluation moments in the replicas' two halves
+    // (models.h stage_derivs); a 16-lane group (N < 16) sums them in one pass at 16 and 64 lanes, so
+    // it is never widened to exactly 32 lanes, where its bits would follow the halves' order
+    if (narrow == 16 && *G == 32) *G = 16;
+  }
 }
 
 template <class Model>

@@ -230,7 +230,9 @@ struct ReplicateOf<M, std::void_t<decltype(M::kReplicate)>> {
 // The stage evaluation of a group of G lanes, one per node (R = 1).  Where the same group may
 // also run replicated -- a replicating model's 32-lane groups, widened to a wave when the batch
 // leaves SIMDs idle (solve_group_size) -- the moments are summed in the replicas' two halves, so an
-// instance gets the same bits whatever batch (and hence group variant) it is solved in.
+// instance gets the same bits whatever batch (and hence group variant) it is solved in.  Every
+// 32-lane launch of such a model is a 16 <= N < 32 group: kernels.h solve_shape never widens a
+// 16-lane group (N < 16, summed in one pass at 16 and 64 lanes) to 32.
 template <class Model, int G, class... Args>
 __device__ __forceinline__ void stage_derivs(Args&&... args) {
   if constexpr (ReplicateOf<Model>::value && G == 32)

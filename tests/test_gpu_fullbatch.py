@@ -5,7 +5,10 @@ the sizes the bench runs, not test-sized batches:
 * config 5 family -- the cart-pole QP of inverted_pendulum_single_shooting_mpctools.py:16,64 at
   N = 100 (two-wave groups, decoupled suffix), B = 2048;
 * config 5 as named -- the cart-pole swing-up, N = 100, B = 2048 (the bench's multiple-shooting
-  closed loop, and the single-shooting formulation of the reference script cold).
+  closed loop, and the single-shooting formulation of the reference script cold);
+* config 4 family -- the LTV lateral lane change at the bench's N = 50, B = 1024 with per-instance
+  device schedules (the 6-state bicycle of config 4 as named runs at B = 1024 in
+  tests/test_gpu_resto.py).
 
 Each: every status <= 1; a 3-step multi-step launch (DeviceLoop.run, the bench's timed path)
 equals 3 lock-step launches bit for bit on the whole batch; and the C++ IPOPT restatement
@@ -182,3 +185,65 @@ def test_config5_swingup_full_batch(mpcx, C):
     # optimum (8.5e-10); rounding between the kernel's and the oracle's derivative assembly, present
     # before this round's kernel changes too
     oracle_sample("config 5 swing-up (single shooting) N=100 B=2048", ss, P, rs, refs, idx, 4, 5, max_iter_differ=1)
+
+
+def test_config4_ltv_full_batch(mpcx):
+    """Config 4 family at the bench's shape: the LTV lateral lane change, N = 50, B = 1024, each
+    instance re-linearised at vref[t] by a per-instance DEVICE schedule that advances every step
+    (Trajectory_tracking_dynamic_model.py:117-145).  A 3-step multi-step launch with the schedule
+    and reference sequences (tabseq, Pseq: bench.py's timed path) equals 3 lock-step launches bit
+    for bit on the whole batch, every status is 0, and each step's solves of a strided sample of 64
+    instances equal the LQ oracle's (oracle/nlp_ref.py lq_solve; parity unpinned beyond it)."""
+    import torch
+
+    from mpcx import dist as mdist
+    from mpcx.device import DeviceLoop
+    from oracle import nlp_ref
+
+    N, B, K = 50, 1024, 3
+    t0, x0, par = mdist.config4_inputs(0, B, N=N)
+    _, _, vref = mdist.lane_change()
+    lin = mpcx.lateral_ltv(N=N, Delta=0.05, vref=vref, per_instance_tab=np.minimum(t0, 499))
+    solver = mpcx.nlpsol("ltv", "mi355x", lin, {"ipopt": {"max_iter": 3000}})
+    tt = np.minimum(t0[None, :] + np.arange(K)[:, None], 499)  # (K, B) instance times
+    refs = np.ascontiguousarray(par[tt].reshape(K, B, -1))
+    tabs = np.ascontiguousarray(np.repeat(tt[:, :, None], N, axis=2).astype(np.int32))
+    P0 = lin.params(x0, par[tt[0]])
+    dr, dt = torch.from_numpy(refs).cuda(), torch.from_numpy(tabs).cuda()
+    idx = np.arange(0, B, B // SAMPLE)
+    lock = DeviceLoop(solver, P0)
+    st_l, it_l = [], []
+    worst = 0.0
+    for t in range(K):
+        x = lock.P[:, 0:4].cpu().numpy()[idx]  # this step's initial states (the plant applied on the device)
+        lock.set_stage_refs(dr[t])
+        lock.set_schedule(dt[t])
+        lock.step()
+        torch.cuda.synchronize()
+        st_l.append(lock.status.cpu().numpy().copy())
+        it_l.append(lock.iters.cpu().numpy().copy())
+        w = lock.w.cpu().numpy()[idx]
+        for i, b in enumerate(idx):
+            j = tt[t, b]
+            _, U_ref, _ = nlp_ref.lq_solve(x[i], lin.A, lin.B, lin.c, lin.W, np.full(N, j), par[j], [-20], [20])
+            u = w[i, 4:4 + 5 * N:5]
+            worst = max(worst, float(np.max(np.abs(u - U_ref[:, 0])) / max(float(np.max(np.abs(U_ref))), 1.0)))
+    print(f"config 4 LTV N=50 B=1024: max sampled input difference from the LQ oracle {worst:.2e} "
+          f"({K} closed-loop steps x {len(idx)} instances)")
+    assert worst <= U_TOL
+    st_l, it_l = np.array(st_l), np.array(it_l)
+    assert np.all(st_l == 0), np.unique(st_l, return_counts=True)
+    # the same K steps as ONE launch with per-step references and device schedules
+    Pseq = np.zeros((K, B, P0.shape[1]))
+    Pseq[:, :, 4:] = refs
+    run = DeviceLoop(solver, P0)
+    run.set_schedule(dt[0])
+    st_r, it_r = run.run(K, Pseq=torch.from_numpy(Pseq).cuda(), tabseq=dt)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st_r.cpu().numpy(), st_l)
+    np.testing.assert_array_equal(it_r.cpu().numpy(), it_l)
+    for n in ("w", "w0", "lam0", "lamx0", "f"):
+        np.testing.assert_array_equal(getattr(run, n).cpu().numpy(), getattr(lock, n).cpu().numpy(), err_msg=n)
+    np.testing.assert_array_equal(run.P[:, 0:4].cpu().numpy(), lock.P[:, 0:4].cpu().numpy())
+    run.set_schedule(None)
+    lock.set_schedule(None)

@@ -400,6 +400,10 @@ def test_launch_shape_names_the_kernel(mpcx):
     assert h.launch_shape(Bw + 1)[:2] == (32, 1)
     h10 = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=10))._h
     assert h10.launch_shape(16)[:2] == (64, 1) and h10.launch_shape(100 * n_simd)[:2] == (16, 1)
+    # a 16-lane group is never widened to exactly 32 lanes (models.h stage_derivs: the 32-lane kernel
+    # sums the evaluation in the replicas' halves)
+    assert h10.launch_shape(n_simd)[:2] == (64, 1) and h10.launch_shape(n_simd + 1)[:2] == (16, 1)
+    assert h10.launch_shape(2 * n_simd)[:2] == (16, 1)
     h30 = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=30))._h  # scan model: never replicated
     assert h30.launch_shape(16) == (64, 1, "void mpcx::solve_kernel<mpcx::UnicycleScanModel, 64, false, 1>"
                                           "(mpcx::SolveArgs)")
@@ -437,6 +441,25 @@ def test_instance_bits_do_not_depend_on_the_batch(mpcx):
     wb = solver.solve_batch(Pn, w0=w0, lam_g0=l0, lam_x0=lx0)
     for n in ("w", "f", "lam_g", "lam_x", "status", "iters"):
         np.testing.assert_array_equal(wa[n], wb[n][:B], err_msg=f"warm {n}")
+
+
+def test_instance_bits_do_not_depend_on_the_batch_short_horizon(mpcx):
+    """The same at N = 10 (16-lane groups): one instance per wave (B <= n_simd, 64 lanes), the
+    batches between n_simd and 2 n_simd (which once ran an unreplicated 32-lane kernel that sums the
+    evaluation in two halves) and four instances per wave give identical bits."""
+    import torch
+
+    from mpcx import dist
+
+    n_simd = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    N, B = 10, n_simd
+    solver = mpcx.nlpsol("s", "mi355x", mpcx.unicycle_point_to_point(N=N))
+    P2 = dist.config2_inputs(0, 3 * B)
+    r_w = solver.solve_batch(P2[:B])
+    for Bb in (B + 1, 2 * B, 3 * B):
+        r_n = solver.solve_batch(P2[:Bb])
+        for n in ("w", "f", "lam_g", "lam_x", "status", "iters"):
+            np.testing.assert_array_equal(r_w[n], r_n[n][:B], err_msg=f"{n} (B={Bb})")
 
 
 def test_max_iter_status(mpcx):
@@ -959,13 +982,25 @@ def test_nonfinite_instance_fails_alone(mpcx):
     np.testing.assert_array_equal(r["iters"][others], ref["iters"][others])
 
 
-def test_bench_two_ranks_rehearsal(tmp_path):
+@pytest.mark.parametrize("workload,B", [
+    ([], 1024),                                       # config 2 (BASELINE metric)
+    (["--config", "4"], 1024),                        # LTV lateral, N = 50: per-instance device schedules
+    (["--config", "4", "--model", "dyn_bicycle"], 1024),  # 6-state bicycle, N = 50, chain stash workspace
+    (["--config", "5"], 2048),                        # cart-pole QP, N = 100: two-wave groups, suffix cache
+], ids=["config2", "config4_ltv", "config4_dyn_bicycle", "config5_qp"])
+def test_bench_two_ranks_rehearsal(tmp_path, workload, B):
     """The multi-rank bench path end to end (torch.distributed.run, 2 ranks, weak
     scaling, stats all_gather, max-over-ranks timing), rehearsed on ONE GPU: both ranks on
     device 0 and gloo collectives (RCCL needs a GPU per rank; the 8-GPU run is the driver's).
     Sharding is exact: the all-gathered per-instance statistics of the
     2-rank run -- final states, objective, statuses, iteration counts of every closed-loop
-    step -- equal, bit for bit, those of ONE rank solving the global instance ids [0, 2B)."""
+    step -- equal, bit for bit, those of ONE rank solving the global instance ids [0, 2B).
+    Every BASELINE config that is sharded over GPUs: config 2, and configs 4 (both models) and 5,
+    whose per-rank state the default config lacks -- the per-instance device schedules of the LTV
+    loop (bench.py tabseq), the 6-state bicycle's chain workspace, the cart-pole QP's multi-wave
+    groups and its per-handle decoupled-suffix cache (one handle per rank against one handle for
+    both shards; Trajectory_tracking_dynamic_model.py:117-145,
+    inverted_pendulum_single_shooting_mpctools.py:16,64)."""
     import json
     import os
     import socket
@@ -980,17 +1015,19 @@ def test_bench_two_ranks_rehearsal(tmp_path):
     env = dict(os.environ, MPCX_FORCE_DEVICE="0", MPCX_DIST_BACKEND="gloo")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    # B per rank = the SIMD count of the MI355X (1024): each rank's launches run replicated 32-lane
-    # groups, the single rank's 2B instances the narrow ones -- the weak-scaling case of the bench
-    B = 1024
-    common = ["--steps", "3", "--warmup", "1", "--no-cpu", "--no-roofline", "--no-reference-warm-start"]
+    # config 2: B per rank = the SIMD count of the MI355X (1024): each rank's launches run replicated
+    # 32-lane groups, the single rank's 2B instances the narrow ones -- the weak-scaling case of the bench
+    common = workload + ["--steps", "3", "--warmup", "1", "--no-cpu", "--no-roofline", "--no-reference-warm-start"]
     flags = ["--gpus", "2", "--batch", str(B)] + common
     launched = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py")] + flags
     plain = [sys.executable, os.path.join(ROOT, "bench.py")] + flags  # bench.py starts its 2 ranks itself
     single = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--batch", str(2 * B)] + common
     stats = {}
-    for name, cmd in (("launched", launched), ("plain", plain), ("single", single)):
+    runs = (("launched", launched), ("plain", plain), ("single", single))
+    if workload:  # the torch.distributed.run launch path is the same for every workload
+        runs = runs[1:]
+    for name, cmd in runs:
         dump = str(tmp_path / f"{name}.npy")
         out = subprocess.run(cmd + ["--dump-stats", dump], env=env if name != "single" else dict(os.environ),
                              capture_output=True, text=True, timeout=600, cwd=ROOT)
@@ -1003,7 +1040,7 @@ def test_bench_two_ranks_rehearsal(tmp_path):
         assert d["failed_instances"] == 0 and d["value"] > 0 and d["steps"] == 3
         stats[name] = np.load(dump)
     assert stats["single"].shape == (2 * B, 8)
-    for name in ("launched", "plain"):
+    for name in stats:
         np.testing.assert_array_equal(stats[name], stats["single"], err_msg=name)
 
 

@@ -39,15 +39,27 @@ def timed_launch(rows):
     return rows[last][1], sum(v for _, _, v in rows[last:]), len(rows) - last
 
 
-def main():
-    from mpcx import _lib
+def profiled_hash(d):
+    """mpcx_source_hash the profiled bench process printed (its stdout, D + '.log', as
+    tools/round_profile.sh writes it): the library that ran under the counters, not the one this
+    script would load."""
+    log = d.rstrip("/") + ".log"
+    for ln in open(log):
+        if ln.startswith("{") and "profile_solve_only" in ln:
+            return json.loads(ln)["mpcx_source_hash"]
+    raise SystemExit(f"{log}: no profile_solve_only line with the source hash")
 
+
+def main():
     fdir, wdir = sys.argv[1], sys.argv[2]
     out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "r05_solve_traffic.json")
     kf, fk, nf = timed_launch(dispatches(fdir, "FETCH_SIZE"))
     kw, wk, nw = timed_launch(dispatches(wdir, "WRITE_SIZE"))
     if kf != kw:
         raise SystemExit(f"passes disagree on the timed kernel: {kf} / {kw}")
+    hf, hw = profiled_hash(fdir), profiled_hash(wdir)
+    if hf != hw:
+        raise SystemExit(f"passes profiled different libraries: {hf} / {hw}")
     rd, wr = 2.0 * fk * 1024, wk * 1024
     d = {"kernel": kf, "dispatches_in_timed_launch": [nf, nw], "fetch_size_kib_raw": fk, "write_size_kib_raw": wk,
          "read_bytes_corrected": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
@@ -55,7 +67,7 @@ def main():
                     "20-step launch)",
          "correction": "FETCH_SIZE x2 (gfx950 counts half of the read bytes; calibrated for 8-B and 16-B per-lane "
                        "loads), WRITE_SIZE x1",
-         "mpcx_source_hash": _lib.source_hash()}
+         "mpcx_source_hash": hf}
     with open(out, "w") as f:
         json.dump(d, f, indent=1)
     print(json.dumps(d))
