@@ -261,31 +261,66 @@ __device__ __forceinline__ void group_next(const double* v, double* out, XWave<G
   }
 }
 
-// acc += (element E of a block-uniform matrix) * w, where lane r of every 16-lane row holds
-// element r of the matrix (m): v_fmac_f64 with a DPP row_newbcast source (gfx950's 64-bit DPP),
-// one instruction, no LDS round trip per element.  The s_nop covers the VALU-write -> DPP-read
-// hazard of m, which the compiler does not see inside the asm.
-template <int E>
-__device__ __forceinline__ void fmac_row_bcast(double& acc, double m, double w) {
-  static_assert(E >= 0 && E < 16, "row lane");
-  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-               : "+v"(acc)
-               : "v"(m), "v"(w), "n"(E));
-}
 // acc[i] += sum_j M[i][j] w[j] (j ascending: the fma order of a plain loop) for an NX x NX matrix
-// held as mA = M[r], mB = M[16 + r] on row lane r (NX <= 5)
-template <int NX, int E>
-__device__ __forceinline__ void matvec_bcast_e(double* acc, const double* w, double mA, double mB) {
-  if constexpr (E < 16)
-    fmac_row_bcast<E>(acc[E / NX], mA, w[E % NX]);
-  else
-    fmac_row_bcast<E - 16>(acc[E / NX], mB, w[E % NX]);
-}
-template <int NX, int... E>
-__device__ __forceinline__ void matvec_bcast(double* acc, const double* w, double mA, double mB,
-                                             std::integer_sequence<int, E...>) {
-  static_assert(NX * NX <= 32, "two row registers");
-  (matvec_bcast_e<NX, E>(acc, w, mA, mB), ...);
+// held as mA = M[r], mB = M[16 + r] on row lane r (NX = 4, 5): ONE asm statement behind ONE s_nop 1
+// (round 5 had an s_nop 1 before each of the NX^2 FMAs: the VALU-write -> DPP-read hazard only concerns
+// mA / mB, which the caller loads from LDS and nothing inside the block writes).  The accumulators
+// are interleaved (j outer, i inner); each one still sums j ascending, so the bits are the plain loop's.
+template <int NX>
+__device__ __forceinline__ void matvec_bcast(double* acc, const double* w, double mA, double mB) {
+  static_assert(NX == 4 || NX == 5, "row-broadcast mat-vec: NX = 4 or 5 (two row registers)");
+  if constexpr (NX == 4) {
+    asm volatile(
+        "s_nop 1\n\t"  // covers a VALU write of mA / mB just before (none is written inside)
+        "v_fmac_f64_dpp %0, %8, %4 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %8, %4 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %8, %4 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %8, %4 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %8, %5 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %8, %5 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %8, %5 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %8, %5 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %8, %6 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %8, %6 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %8, %6 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %8, %6 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %8, %7 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %8, %7 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %8, %7 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %8, %7 row_newbcast:15 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+        : "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(mA), "v"(mB));
+  } else {
+    asm volatile(
+        "s_nop 1\n\t"  // covers a VALU write of mA / mB just before (none is written inside)
+        "v_fmac_f64_dpp %0, %10, %5 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %5 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %10, %5 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %10, %5 row_newbcast:15 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %11, %5 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %10, %6 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %6 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %10, %6 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %11, %6 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %11, %6 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %10, %7 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %7 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %10, %7 row_newbcast:12 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %11, %7 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %11, %7 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %10, %8 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %8 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %10, %8 row_newbcast:13 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %11, %8 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %11, %8 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %10, %9 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %9 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %10, %9 row_newbcast:14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %11, %9 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %11, %9 row_newbcast:8 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4])
+        : "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(mA), "v"(mB));
+  }
 }
 
 // 1/x to full fp64 accuracy: v_rcp_f64 + two Newton steps (no IEEE division sequence

@@ -32,6 +32,7 @@
 #include "ode.h"
 #include "pscan.h"
 #include "riccati.h"
+#include "rowchain.h"
 #include "solver.h"
 
 // Diagnostic build only (-DMPCX_STAMPS, `make stamps`): per-phase s_memtime cycle
@@ -237,6 +238,17 @@ struct LdsCol {
   __device__ __forceinline__ void relaunder() { asm volatile("" : "+v"(off)); }
 };
 
+// Model::kRowChain if the model declares it: its sequential Riccati recursion runs as the row chain
+// (rowchain.h) in the single-wave groups of 32 and 64 lanes
+template <class M, class = void>
+struct RowChainOf {
+  static constexpr bool value = false;
+};
+template <class M>
+struct RowChainOf<M, std::void_t<decltype(M::kRowChain)>> {
+  static constexpr bool value = M::kRowChain;
+};
+
 // R = 2 (replicated groups, G = 32): a batch too small to give every SIMD a wave runs one
 // instance per wave with its lane group held TWICE, in the wave's two 32-lane halves (replica rho
 // = lane / 32).  Both replicas compute the same bits (every collective is a 32-lane group
@@ -265,6 +277,9 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   // the matrix powers (A^T)^(j 4^l), j = 1..3, l < 5, kept for the launch (table index pow_tab)
   __shared__ double dscan[DecSuffixOf<Model>::value && G > 64 ? 2 * NX * kSBS + 15 * NX * NX : 1];
   double pow_tab = -1.0;  // table whose powers dscan holds (block-uniform)
+  // the row chain's node records (rowchain.h): G records per instance of the wave
+  constexpr bool kRow = RowChainOf<Model>::value && rowchain::fits<Model>() && G >= 32 && G * R <= 64;
+  __shared__ double rcbuf[kRow ? (64 / (G * R)) * G * rowchain::kRec : 1];
   // workspace chain stash (solver.h chain_ws_slots): slots after the restoration workspace's
   constexpr bool kWsStash = WsStashOf<Model>::value;
   // The stash is one contiguous record per thread (array of structures, after the restoration
@@ -1175,7 +1190,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
       };
       stash(false);
       if (__any(seq)) {  // sequential recursion (models without the scan, or its fallback)
-        if (seq) {
+        if (seq && !kRow) {  // (the row chain sets P, p after its chain: not live across it)
           okl = true;
           const double dl = (k == N) ? 1.0 : 0.0;  // P_N = Sigma_x + delta, p_N = barrier gradient
 #pragma unroll
@@ -1294,7 +1309,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
                     w[i] = cur[i * kSBS + src];
                     acc[i] = v[i];
                   }
-                  matvec_bcast<NX>(acc, w, mA, mB, std::make_integer_sequence<int, NX * NX>{});
+                  matvec_bcast<NX>(acc, w, mA, mB);
 #pragma unroll
                   for (int i = 0; i < NX; ++i) v[i] = on ? acc[i] : v[i];
                 }
@@ -1313,7 +1328,67 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
           }
         }
         STAMP_SUB(12);
-        if constexpr (G <= 64) {
+        if constexpr (kRow) {
+          // the row chain (rowchain.h): the node lanes hand their stages to LDS records, every row runs
+          // its instance's whole recursion, and node lane k takes step k's results back -- the same
+          // operations as riccati_step below, so the same bits
+          static_assert(!kDec && !kWsStash, "row chain: plain sequential recursion only");
+          int rslot = (int)((threadIdx.x & 63) / (G * R)) * G * rowchain::kRec;
+          asm volatile("" : "+v"(rslot));  // (not hoisted out of the solve loop: one register less there)
+          double* rinst = rcbuf + rslot;
+          // P_N = Sigma_x + delta, p_N = barrier gradient (node N's value function)
+          auto terminal = [&](double* Pt, double* pt) __attribute__((always_inline)) {
+            const double dl = (k == N) ? 1.0 : 0.0;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+#pragma unroll
+              for (int j = i; j < NX; ++j) Pt[symix(i, j, NX)] = (i == j) ? dl * (sgv[i] + delta) : 0.0;
+              pt[i] = dl * gp[i];
+            }
+          };
+          if (seq && (R == 1 || rho == 0)) {
+            if (hasU) {
+              rowchain::store_stage(rinst + k * rowchain::kRec, Hd, gp, Aop, Bop, cdef);
+            } else if (hasX && k == N) {
+              double PN[NP], pN[NX];
+              terminal(PN, pN);
+              rowchain::store_terminal(rinst + k * rowchain::kRec, PN, pN);
+            }
+          }
+          // one wave per workgroup (G R <= 64): its LDS accesses complete in issue order, so the
+          // hand-overs need only a compiler barrier, no s_barrier and no wait for the stores
+          static_assert(G * R <= 64, "row chain: single-wave workgroups");
+          asm volatile("" ::: "memory");
+          STAMP_SUB(11);  // (diagnostic build: the chain itself as sub-phase 11, unused by this model)
+          rowchain::run<G * R>(rinst, N);
+          asm volatile("" ::: "memory");
+          STAMP_SUB(12);
+          // every node redoes its own step from node k+1's value function -- the chain's step k, the
+          // same function on the same operands -- for its factors and P_k, all nodes at once.  P, p and
+          // the factors are (re)set only here, so none of them is live across the chain (node N and
+          // the lanes past it: P_N / zeros and no factors, as the sequential recursion leaves them),
+          // and the stage Hessian is formed again from its parts (the delta barrier keeps the compiler
+          // from holding the pre-chain copy across the chain instead)
+          if (seq) {
+            if (hasU) {
+              double Pin_[NP], pin_[NX], Hk[NH];
+              rowchain::load_next(rinst + (k + 1) * rowchain::kRec, Pin_, pin_);
+              double dlt = delta;
+              asm volatile("" : "+v"(dlt));
+              const double* Hsrc = Model::hessW(ctx, Hs);
+#pragma unroll
+              for (int i = 0; i < NH; ++i) Hk[i] = Hsrc[i];
+#pragma unroll
+              for (int i = 0; i < NZ; ++i) Hk[symix(i, i, NZ)] += sgv[i] + dlt;
+              (void)riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, false, AOneOf<Model>::value>(
+                  Hk, gp, Aop, Bop, cdef, Pin_, pin_, P, p, fac);
+            } else {
+              terminal(P, p);
+              fac = Fac<NX, NU>{};
+            }
+            okl = !hasU || fac_ok<NX, NU>(fac);
+          }
+        } else if constexpr (G <= 64) {
           if constexpr (kDec) {
             for (int j = N - 1; j >= jc; --j) {
               double pin_[NX];

@@ -43,6 +43,9 @@ struct UnicycleModel {
   // a 32-lane group widened to a whole wave runs as two replicas that split the sequential work
   // (kernels.h R = 2): configs 1-2 (N <= 30) at batches below two waves per SIMD
   static constexpr bool kReplicate = true;
+  // the sequential Riccati recursion spread over 16-lane rows (rowchain.h; bit-identical to
+  // riccati_step) in the single-wave groups of 32 and 64 lanes
+  static constexpr bool kRowChain = true;
   struct Ctx {
     double xr[3], ur[2];
   };
@@ -104,6 +107,7 @@ struct UnicycleFreeModel : UnicycleModel {
 struct UnicycleScanModel : UnicycleModel {
   static constexpr bool kParallelRiccati = true;
   static constexpr bool kReplicate = false;  // no sequential chain to split
+  static constexpr bool kRowChain = false;   // the chain is the scan's rare fallback
 };
 
 // ------------------------------------------------------------------------------------

@@ -23,7 +23,7 @@ __global__ __launch_bounds__(64) void bcast_check_kernel(const double* M, const 
   const int r = t & 15;
   const double mA = Mb[r];
   const double mB = NX * NX > 16 ? Mb[16 + min(r, NX * NX - 17)] : 0.0;
-  matvec_bcast<NX>(a, wl, mA, mB, std::make_integer_sequence<int, NX * NX>{});
+  matvec_bcast<NX>(a, wl, mA, mB);
 #pragma unroll
   for (int i = 0; i < NX; ++i)
 #pragma unroll

@@ -1,0 +1,90 @@
+"""rowchain.h -- the unicycle's backward Riccati recursion spread over 16-lane rows (the solve
+kernel's chain for configs 1-2) -- against the sequential recursion it replaced (riccati_step on
+node lane j, the value function moved lane to lane by DPP), through tests/hip/rowchain_check.hip:
+bit for bit the same P_k, p_k and factors (r0, t, r1, h0, h1, g0, g1) at every node, for the
+unicycle's Jacobian structure with random stage Hessians (indefinite reduced Huu' included),
+random defects and terminal value functions, in the three lane-group shapes that run it (32-lane
+groups two per wave, 32-lane groups replicated, one 64-lane group per wave), N from 1 to G - 1."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hip", "librowchain_check.so")
+K_IN, K_OUT = 47, 22
+
+
+def stages(rng, B, G, scale):
+    """Random unicycle stages: A = I + a02 e0 e2^T + a12 e1 e2^T, B with B[2][0] = 0, symmetric
+    stage Hessians (some with an indefinite u block), barrier gradients, defects, and a terminal
+    value function at every node (the kernel reads node N's only)."""
+    x = np.zeros((B, G, K_IN))
+    Hf = rng.standard_normal((B, G, 5, 5)) * scale[..., None, None]
+    Hf = Hf @ np.swapaxes(Hf, -1, -2) + np.eye(5) * rng.uniform(0.0, 2.0, (B, G, 1, 1))
+    Hf[:, ::7, 3:, 3:] -= 4.0 * np.eye(2)  # every 7th stage: an indefinite control block
+    iu = [(i, j) for i in range(5) for j in range(i, 5)]
+    x[..., 0:15] = np.stack([Hf[..., i, j] for i, j in iu], axis=-1)
+    x[..., 15:20] = rng.standard_normal((B, G, 5)) * scale[..., None]
+    A = np.broadcast_to(np.eye(3), (B, G, 3, 3)).copy()
+    A[..., 0, 2], A[..., 1, 2] = rng.standard_normal((2, B, G)) * 0.2
+    Bm = rng.standard_normal((B, G, 3, 2)) * 0.2
+    Bm[..., 2, 0] = 0.0
+    x[..., 20:29] = A.reshape(B, G, 9)
+    x[..., 29:35] = Bm.reshape(B, G, 6)
+    x[..., 35:38] = rng.standard_normal((B, G, 3)) * 1e-2
+    Pf = rng.standard_normal((B, G, 3, 3))
+    Pf = Pf @ np.swapaxes(Pf, -1, -2) + np.eye(3)
+    x[..., 38:44] = np.stack([Pf[..., i, j] for i in range(3) for j in range(i, 3)], axis=-1)
+    x[..., 44:47] = rng.standard_normal((B, G, 3))
+    return x
+
+
+@pytest.mark.parametrize("G,R,N", [(32, 1, 20), (32, 1, 1), (32, 1, 31), (32, 2, 20), (32, 2, 16),
+                                   (64, 1, 10), (64, 1, 63)])
+def test_row_chain_is_the_sequential_recursion(G, R, N):
+    import torch
+
+    if not os.path.exists(LIB):
+        pytest.fail(f"{LIB} not built (make -C tests/hip)")
+    lib = ctypes.CDLL(LIB)
+    lib.rowchain_check.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p] * 4
+    B = 257 if R == 1 else 128  # an odd batch: the last wave's second 32-lane group is empty
+    rng = np.random.default_rng(1000 * G + 10 * N + R)
+    scale = np.exp(rng.uniform(-3, 3, (B, G)))  # magnitudes 1e-1 .. 1e1 per stage
+    x = stages(rng, B, G, scale)
+    d_in = torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    o_seq = torch.full((B, G, K_OUT), np.nan, dtype=torch.float64, device="cuda")
+    o_row = torch.full_like(o_seq, np.nan)
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    waves = (B * G * R + 63) // 64
+    cyc = torch.zeros(2 * waves, dtype=torch.int64, device="cuda")
+    assert lib.rowchain_check(G, R, N, B, ptr(d_in), ptr(o_seq), ptr(o_row), ptr(cyc)) == 0
+    c = cyc.cpu().numpy().reshape(waves, 2)
+    print(f"G={G} R={R} N={N}: cycles per step, sequential recursion {c[:, 0].mean() / N:.0f}, "
+          f"row chain {c[:, 1].mean() / N:.0f}")
+    a, b = o_seq.cpu().numpy()[:, :N + 1], o_row.cpu().numpy()[:, :N + 1]
+    assert np.isfinite(a[:, :N, :20]).mean() > 0.5  # the recursion ran (indefinite stages may overflow)
+    np.testing.assert_array_equal(b.view(np.int64), a.view(np.int64))
+    # and it is a Riccati recursion: node N-1's P from the formula in numpy (rtol, not bits; node N-1
+    # of N = 1 is a stage with an indefinite control block by construction)
+    if (N - 1) % 7 == 0:
+        return
+    s = x[:, N - 1]
+    Hf = np.zeros((B, 5, 5))
+    for q, (i, j) in enumerate([(i, j) for i in range(5) for j in range(i, 5)]):
+        Hf[:, i, j] = Hf[:, j, i] = s[:, q]
+    A, Bm, c = s[:, 20:29].reshape(B, 3, 3), s[:, 29:35].reshape(B, 3, 2), s[:, 35:38]
+    PN = np.zeros((B, 3, 3))
+    for q, (i, j) in enumerate([(i, j) for i in range(3) for j in range(i, 3)]):
+        PN[:, i, j] = PN[:, j, i] = x[:, N, 38 + q]
+    W = np.concatenate([A, Bm], axis=2)
+    Q = Hf + np.swapaxes(W, 1, 2) @ PN @ W
+    Pk = Q[:, :3, :3] - Q[:, :3, 3:] @ np.linalg.solve(Q[:, 3:, 3:], Q[:, 3:, :3])
+    got = np.stack([b[:, N - 1, q] for q in range(6)], axis=-1)
+    want = np.stack([Pk[:, i, j] for i in range(3) for j in range(i, 3)], axis=-1)
+    ok = np.all(np.linalg.eigvalsh(Q[:, 3:, 3:]) > 1e-6, axis=1)
+    assert ok.sum() > B // 2
+    np.testing.assert_allclose(got[ok], want[ok], rtol=1e-8, atol=1e-8 * np.abs(want[ok]).max())
