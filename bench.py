@@ -46,8 +46,8 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # FP64 vector (VALU) peak: AMD's MI355X spec, half the FP32 vector peak of 157.3 TF/s
 # (MI355X_MICROARCH.md); the solve kernel issues scalar-per-lane FP64 FMAs, no MFMA
 PEAK_FP64_TFLOPS = 78.6
-SOLVE_PMC = os.path.join("profiles", "r05_solve_kernel_pmc.json")
-SOLVE_TRAFFIC = "r05_solve_traffic.json"  # HBM bytes of the timed launch (tools/solve_traffic.py)
+SOLVE_PMC = os.path.join("profiles", "r06_solve_kernel_pmc.json")
+SOLVE_TRAFFIC = "r06_solve_traffic.json"  # HBM bytes of the timed launch (tools/solve_traffic.py)
 SWEEP_BYTES_PER_STAGE = 256  # read x_k,u_k,x_{k+1} (64 B) + write c,q,A,B,grad q (192 B)
 SWEEP_BYTES_PER_INSTANCE = 48  # P
 
@@ -685,6 +685,8 @@ def main():
                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic,
                 "launch_ms": round(ms, 4), "units_per_launch": Br * N, "unit_of_work": "stage evaluation",
                 "bytes_per_launch": alg, "config": f"B={Br}, N={N}"}
+        if traffic:  # the HBM rate the launch actually moved (PMC bytes, compulsory writes included)
+            roof["frac_on_traffic"] = round(traffic / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
 
     # the dominant kernel of the timed region: the multi-step solve launch (async mode; HIP
     # events on the launch stream) or the mean single-step launch (lock-step latency run)

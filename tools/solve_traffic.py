@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """HBM bytes of the bench's timed K-step solve launch from two rocprofv3 PMC passes
-(profiles/r05_solve_traffic.json; bench.py reads it into roofline.traffic while the tree's
+(profiles/r06_solve_traffic.json; bench.py reads it into roofline.traffic while the tree's
 sources still hash to the ones measured).
 
     python tools/solve_traffic.py FETCH_DIR WRITE_DIR [OUT]
@@ -52,7 +52,7 @@ def profiled_hash(d):
 
 def main():
     fdir, wdir = sys.argv[1], sys.argv[2]
-    out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "r05_solve_traffic.json")
+    out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "r06_solve_traffic.json")
     kf, fk, nf = timed_launch(dispatches(fdir, "FETCH_SIZE"))
     kw, wk, nw = timed_launch(dispatches(wdir, "WRITE_SIZE"))
     if kf != kw:
