@@ -33,6 +33,7 @@
 #include "pscan.h"
 #include "riccati.h"
 #include "rowchain.h"
+#include "rowchain6.h"
 #include "solver.h"
 
 // Diagnostic build only (-DMPCX_STAMPS, `make stamps`): per-phase s_memtime cycle
@@ -271,8 +272,12 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   // LDS buffer of the Riccati scan (pscan.h): one element per thread, structure of arrays
   constexpr int kSBS = G > 64 ? G : 64;  // threads per block = field stride
   __shared__ double sbuf[Model::kParallelRiccati ? RElem<NX>::NE * kSBS : 1];
+  // the 6-state row chain (rowchain6.h): one instance per wave, its node records in an LDS ring
+  // that aliases the transcendental cache (idle during the Riccati phase)
+  constexpr bool kRow6 = RowChainOf<Model>::value && rowchain6::fits<Model>() && G == 64 && R == 1;
   // LDS cache of the ODE models' transcendental values across their derivative passes (ode.h)
-  __shared__ double tcache[Model::kTrigSlots > 0 ? Model::kTrigSlots * kSBS : 1];
+  constexpr int kTcache = Model::kTrigSlots > 0 ? Model::kTrigSlots * kSBS : 1;
+  __shared__ double tcache[kRow6 && rowchain6::kRing > kTcache ? rowchain6::kRing : kTcache];
   // the decoupled suffix's vector scan (multi-wave groups): two NX-double buffers per thread, then
   // the matrix powers (A^T)^(j 4^l), j = 1..3, l < 5, kept for the launch (table index pow_tab)
   __shared__ double dscan[DecSuffixOf<Model>::value && G > 64 ? 2 * NX * kSBS + 15 * NX * NX : 1];
@@ -287,8 +292,8 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   // a few cache lines in 16-byte loads instead of one line per value.
   constexpr int kWsH = RestoWs::slots(NX, NU);  // slot-major slots before the records
   constexpr int kCS = chain_ws_slots(NX, NU);   // record: stage Hessian (NH), Sigma (NZ), A (NX^2), B (NX NU)
-  constexpr int kRH = 0, kRS = NH, kRA = NH + NZ, kRB = NH + NZ + NX * NX;
-  static_assert(!kWsStash || (kRB + NX * NU == kCS && kCS % 2 == 0), "chain stash record");
+  constexpr int kRH = 0, kRS = NH, kRA = NH + NZ, kRB = NH + NZ + NX * NX, kRP = kRB + NX * NU;
+  static_assert(!kWsStash || (kRP + (NX + 1) * NX == kCS && kCS % 2 == 0), "chain stash record");
   // this thread's record (16-byte aligned: hipMalloc base, 64-thread-multiple stride, even kCS);
   // opaque, so no address is hoisted out of the solve loop
   auto wsrec = [&]() __attribute__((always_inline)) -> const double* {
@@ -1168,7 +1173,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
       // Stash: the iterate, its bound multipliers, bounds and lam are live across the sequential
       // chain but unused in it; for the 6-state model they go to the LDS value cache (idle
       // between evaluations) so the chain's operands keep registers instead of scratch
-      constexpr bool kStash = !Model::kParallelRiccati && NX >= 6 && Model::kTrigSlots >= 5 * NZ + NX;
+      constexpr bool kStash = !Model::kParallelRiccati && NX >= 6 && Model::kTrigSlots >= 5 * NZ + NX && !kRow6;
       auto stash = [&](bool back) __attribute__((always_inline)) {
         if constexpr (kStash) {
           double* t = tcache + threadIdx.x;
@@ -1190,7 +1195,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
       };
       stash(false);
       if (__any(seq)) {  // sequential recursion (models without the scan, or its fallback)
-        if (seq && !kRow) {  // (the row chain sets P, p after its chain: not live across it)
+        if (seq && !kRow && !kRow6) {  // (the row chains set P, p after the chain: not live across it)
           okl = true;
           const double dl = (k == N) ? 1.0 : 0.0;  // P_N = Sigma_x + delta, p_N = barrier gradient
 #pragma unroll
@@ -1384,6 +1389,61 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
                   Hk, gp, Aop, Bop, cdef, Pin_, pin_, P, p, fac);
             } else {
               terminal(P, p);
+              fac = Fac<NX, NU>{};
+            }
+            okl = !hasU || fac_ok<NX, NU>(fac);
+          }
+        } else if constexpr (kRow6) {
+          // the 6-state row chain (rowchain6.h): the node lanes write their stages (from the
+          // workspace stash) into the LDS ring window by window, every row runs the instance's
+          // recursion and stores each node's value function into that node's workspace slots, and
+          // node lane k redoes its own step from node k+1's -- the chain's step k, the same
+          // operations as riccati_step, so the same bits -- for its factors and P_k.  Without the
+          // sequential chain's early stop: a failed step still fails the attempt (fac_ok below)
+          static_assert(!kDec && kWsStash, "6-state row chain: plain sequential recursion, workspace stash");
+          auto fill = [&](int lo, int hi, bool top) __attribute__((always_inline)) {
+            if (seq && hasU && k >= lo && k <= hi) {
+              const double* r = wsrec();
+              double Hs_[NH], sg_[NZ], A_[NX * NX], B_[NX * NU];
+#pragma unroll
+              for (int i = 0; i < NH; ++i) Hs_[i] = wsload(r, kRH + i);
+#pragma unroll
+              for (int i = 0; i < NZ; ++i) sg_[i] = wsload(r, kRS + i);
+              ws_jac(A_, B_);
+              rowchain6::store_node(tcache + (k - lo) * rowchain6::kRec, Hs_, sg_, delta, A_, B_, gp, cdef);
+            }
+            if (top && seq && hasX && k == N)
+              rowchain6::store_terminal(tcache + (N - lo) * rowchain6::kRec, sgv, delta, gp);
+          };
+          double* out0 = a.ws + (long)kWsH * a.ws_stride + (gid - k) * kCS + kRP;  // node 0's slots
+          STAMP_SUB(11);
+          rowchain6::run(tcache, out0, kCS, valid && seq, N, fill);
+          __syncthreads();  // row 0's workspace stores, before the node lanes read them
+          STAMP_SUB(12);
+          if (seq) {
+            if (hasU) {
+              double Pin_[NP], pin_[NX], Hj[NH], Aj[NX * NX], Bj[NX * NU];
+              rowchain6::load_next(wsrec() + kCS + kRP, Pin_, pin_);
+              ws_jac(Aj, Bj);
+              const double* r = wsrec();
+#pragma unroll
+              for (int i = 0; i < NZ; ++i)
+#pragma unroll
+                for (int jj = i; jj < NZ; ++jj) {
+                  const int t = symix(i, jj, NZ);
+                  Hj[t] = wsload(r, kRH + t);
+                  if (jj == i) Hj[t] += wsload(r, kRS + i) + delta;
+                }
+              (void)riccati_step<NX, NU, Model::AMASK, Model::BMASK, false, false, AOneOf<Model>::value>(
+                  Hj, gp, Aj, Bj, cdef, Pin_, pin_, P, p, fac);
+            } else {
+              const double dl = (k == N) ? 1.0 : 0.0;  // node N: P_N = Sigma_x + delta, p_N = gradient
+#pragma unroll
+              for (int i = 0; i < NX; ++i) {
+#pragma unroll
+                for (int j = i; j < NX; ++j) P[symix(i, j, NX)] = (i == j) ? dl * (sgv[i] + delta) : 0.0;
+                p[i] = dl * gp[i];
+              }
               fac = Fac<NX, NU>{};
             }
             okl = !hasU || fac_ok<NX, NU>(fac);

@@ -426,6 +426,8 @@ struct OdeModel {
   // already wait in the workspace, 3 % slower -- so not there
   static constexpr bool kBoundsLds = NX < 6;
   static constexpr bool kParallelRiccati = NX <= 5;  // NX = 6: LDS buffer too large
+  // the 6-state model's chain runs spread over 16-lane rows (rowchain6.h; one instance per wave)
+  static constexpr bool kRowChain = NX == 6;
   struct Ctx {
     double zr[NZ];
   };

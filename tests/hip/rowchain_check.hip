@@ -8,6 +8,7 @@
 // from each node's own step redone on the chain's value functions, as in the solve kernel.  Built into tests/hip/librowchain_check.so
 // (tests/hip/Makefile); used by tests/test_gpu_rowchain.py only.
 #include "kernels.h"
+#include "rowchain6.h"
 
 namespace mpcx {
 
@@ -102,7 +103,99 @@ __global__ __launch_bounds__(64) void rowchain_check_kernel(int N, int B, const 
   }
 }
 
+// ---- the 6-state chain (rowchain6.h): one instance per 64-lane wave, window by window
+// in, per node (64 per instance): Hs 36 (packed upper, 8x8), Sigma 8, A 36, B 12, gp 8, c 6
+constexpr int kIn6 = 106, kOut6 = 21 + 6 + 17;
+
+__device__ void put_out6(double* o, const double* P, const double* p, const Fac<6, 2>& f) {
+  for (int i = 0; i < 21; ++i) o[i] = P[i];
+  for (int i = 0; i < 6; ++i) o[21 + i] = p[i];
+  o[27] = f.r0;
+  o[28] = f.t;
+  o[29] = f.r1;
+  for (int i = 0; i < 6; ++i) {
+    o[30 + i] = f.h0[i];
+    o[36 + i] = f.h1[i];
+  }
+  o[42] = f.g0;
+  o[43] = f.g1;
+}
+
+__global__ __launch_bounds__(64) void rowchain6_check_kernel(int N, double delta, const double* in, double* ws,
+                                                             double* out_seq, double* out_row, unsigned long long* cyc) {
+  namespace rc = rowchain6;
+  constexpr unsigned long long AM = rc::amask6(), BM = (1ull << 12) - 1;
+  __shared__ double ring[rc::kRing];
+  const int k = (int)threadIdx.x;
+  const long inst = blockIdx.x;
+  double Hs[36] = {}, sig[8] = {}, A[36] = {}, Bm[12] = {}, gp[8] = {}, c[6] = {};
+  if (k <= N) {
+    const double* r = in + (inst * 64 + k) * kIn6;
+    for (int i = 0; i < 36; ++i) Hs[i] = r[i];
+    for (int i = 0; i < 8; ++i) sig[i] = r[36 + i];
+    for (int i = 0; i < 36; ++i) A[i] = r[44 + i];
+    for (int i = 0; i < 12; ++i) Bm[i] = r[80 + i];
+    for (int i = 0; i < 8; ++i) gp[i] = r[92 + i];
+    for (int i = 0; i < 6; ++i) c[i] = r[100 + i];
+  }
+  double Hd[36];
+  for (int i = 0; i < 36; ++i) Hd[i] = Hs[i];
+  for (int i = 0; i < 8; ++i) Hd[symix(i, i, 8)] += sig[i] + delta;  // the solve kernel's order
+  // ---- the sequential recursion (node lane j runs step j)
+  double P[21], p[6];
+  for (int i = 0; i < 6; ++i) {
+    for (int j = i; j < 6; ++j) P[symix(i, j, 6)] = (k == N && i == j) ? sig[i] + delta : 0.0;
+    p[i] = k == N ? gp[i] : 0.0;
+  }
+  Fac<6, 2> fac = {};
+  const unsigned long long t0 = clk();
+  for (int j = N - 1; j >= 0; --j) {
+    double Pin_[21], pin_[6];
+    for (int i = 0; i < 21; ++i) Pin_[i] = from_next(P[i]);
+    for (int i = 0; i < 6; ++i) pin_[i] = from_next(p[i]);
+    if (k == j) (void)riccati_step<6, 2, AM, BM, false, false, 0>(Hd, gp, A, Bm, c, Pin_, pin_, P, p, fac);
+  }
+  const unsigned long long t1 = clk();
+  if (k <= N) put_out6(out_seq + (inst * 64 + k) * kOut6, P, p, fac);
+  // ---- the row chain, then every node's own step from the chain's value functions
+  auto fill = [&](int lo, int hi, bool top) __attribute__((always_inline)) {
+    if (k >= lo && k <= hi) rc::store_node(ring + (k - lo) * rc::kRec, Hs, sig, delta, A, Bm, gp, c);
+    if (top && k == N) rc::store_terminal(ring + (N - lo) * rc::kRec, sig, delta, gp);
+  };
+  double* out0 = ws + inst * 64 * rc::kOut;
+  const unsigned long long t2 = clk();
+  rc::run(ring, out0, rc::kOut, true, N, fill);
+  const unsigned long long t3 = clk();
+  __syncthreads();
+  double P2[21], p2[6];
+  Fac<6, 2> fac2 = {};
+  if (k < N) {
+    double Pin_[21], pin_[6];
+    rc::load_next(out0 + (k + 1) * rc::kOut, Pin_, pin_);
+    (void)riccati_step<6, 2, AM, BM, false, false, 0>(Hd, gp, A, Bm, c, Pin_, pin_, P2, p2, fac2);
+  } else {
+    for (int i = 0; i < 6; ++i) {
+      for (int j = i; j < 6; ++j) P2[symix(i, j, 6)] = (k == N && i == j) ? sig[i] + delta : 0.0;
+      p2[i] = k == N ? gp[i] : 0.0;
+    }
+  }
+  if (k <= N) put_out6(out_row + (inst * 64 + k) * kOut6, P2, p2, fac2);
+  if (cyc && k == 0) {
+    cyc[2 * blockIdx.x] = t1 - t0;
+    cyc[2 * blockIdx.x + 1] = t3 - t2;
+  }
+}
+
 }  // namespace mpcx
+
+// in: B * 64 * 106 doubles (node records, nodes 0..N used); ws: B * 64 * kOut scratch; outputs
+// B * 64 * 44 doubles each; cyc (may be null): per wave the cycles of the two chains
+extern "C" int rowchain6_check(int N, int B, double delta, const double* in, double* ws, double* out_seq,
+                               double* out_row, unsigned long long* cyc) {
+  if (B <= 0 || N < 1 || N > 63) return 1;
+  hipLaunchKernelGGL(mpcx::rowchain6_check_kernel, dim3(B), dim3(64), 0, 0, N, delta, in, ws, out_seq, out_row, cyc);
+  return hipDeviceSynchronize() == hipSuccess ? 0 : 3;
+}
 
 // G = 32 (R = 1: two instances per wave; R = 2: one, replicated) or 64; in: B * G * 47 doubles,
 // outputs B * G * 22 doubles each, cyc (may be null): per wave the cycles of the sequential recursion

@@ -88,3 +88,69 @@ def test_row_chain_is_the_sequential_recursion(G, R, N):
     ok = np.all(np.linalg.eigvalsh(Q[:, 3:, 3:]) > 1e-6, axis=1)
     assert ok.sum() > B // 2
     np.testing.assert_allclose(got[ok], want[ok], rtol=1e-8, atol=1e-8 * np.abs(want[ok]).max())
+
+
+# ---- rowchain6.h: the 6-state bicycle's chain (one instance per 64-lane wave, window by window)
+K_IN6, K_OUT6, K_WS6 = 106, 44, 42
+IU8 = [(i, j) for i in range(8) for j in range(i, 8)]
+
+
+def stages6(rng, B, delta):
+    """Random 6-state stages with the model's Jacobian structure (columns x0, x1 of A unit
+    vectors, the rest dense; B dense), symmetric stage Hessians (every 7th stage with an
+    indefinite control block), Sigma, gradients and defects at all 64 nodes."""
+    x = np.zeros((B, 64, K_IN6))
+    Hf = rng.standard_normal((B, 64, 8, 8)) * 0.5
+    Hf = Hf @ np.swapaxes(Hf, -1, -2) + np.eye(8) * rng.uniform(0.0, 2.0, (B, 64, 1, 1))
+    Hf[:, 3::7, 6:, 6:] -= 6.0 * np.eye(2)
+    x[..., 0:36] = np.stack([Hf[..., i, j] for i, j in IU8], axis=-1)
+    x[..., 36:44] = rng.uniform(0.0, 1.0, (B, 64, 8))
+    A = np.eye(6) + rng.standard_normal((B, 64, 6, 6)) * 0.2
+    A[..., :, 0] = np.eye(6)[:, 0]
+    A[..., :, 1] = np.eye(6)[:, 1]
+    x[..., 44:80] = A.reshape(B, 64, 36)
+    x[..., 80:92] = (rng.standard_normal((B, 64, 6, 2)) * 0.2).reshape(B, 64, 12)
+    x[..., 92:100] = rng.standard_normal((B, 64, 8))
+    x[..., 100:106] = rng.standard_normal((B, 64, 6)) * 1e-2
+    return x
+
+
+@pytest.mark.parametrize("N,delta", [(50, 0.0), (50, 1e-4), (35, 0.0), (36, 0.0), (63, 0.0), (1, 0.0), (12, 3e-3)])
+def test_row_chain6_is_the_sequential_recursion(N, delta):
+    import torch
+
+    if not os.path.exists(LIB):
+        pytest.fail(f"{LIB} not built (make -C tests/hip)")
+    lib = ctypes.CDLL(LIB)
+    lib.rowchain6_check.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double] + [ctypes.c_void_p] * 5
+    B = 96
+    rng = np.random.default_rng(7 * N + 1)
+    x = stages6(rng, B, delta)
+    d_in = torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    ws = torch.full((B, 64, K_WS6), np.nan, dtype=torch.float64, device="cuda")
+    o_seq = torch.full((B, 64, K_OUT6), np.nan, dtype=torch.float64, device="cuda")
+    o_row = torch.full_like(o_seq, np.nan)
+    cyc = torch.zeros(2 * B, dtype=torch.int64, device="cuda")
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    assert lib.rowchain6_check(N, B, delta, ptr(d_in), ptr(ws), ptr(o_seq), ptr(o_row), ptr(cyc)) == 0
+    c = cyc.cpu().numpy().reshape(B, 2)
+    print(f"N={N}: cycles per step, sequential recursion {c[:, 0].mean() / N:.0f}, row chain {c[:, 1].mean() / N:.0f}")
+    a, b = o_seq.cpu().numpy()[:, :N + 1], o_row.cpu().numpy()[:, :N + 1]
+    assert np.isfinite(a[:, :N, :27]).mean() > 0.5
+    np.testing.assert_array_equal(b.view(np.int64), a.view(np.int64))
+    # a Riccati recursion: node N-1's P_{N-1} from the formula (a stage with a definite control block)
+    if (N - 1) % 7 == 3:
+        return
+    s = x[:, N - 1]
+    Hf = np.zeros((B, 8, 8))
+    for q, (i, j) in enumerate(IU8):
+        Hf[:, i, j] = Hf[:, j, i] = s[:, q]
+    Hf += np.einsum("bi,ij->bij", s[:, 36:44] + delta, np.eye(8))
+    A, Bm = s[:, 44:80].reshape(B, 6, 6), s[:, 80:92].reshape(B, 6, 2)
+    PN = np.einsum("bi,ij->bij", x[:, N, 36:42] + delta, np.eye(6))
+    W = np.concatenate([A, Bm], axis=2)
+    Q = Hf + np.swapaxes(W, 1, 2) @ PN @ W
+    Pk = Q[:, :6, :6] - Q[:, :6, 6:] @ np.linalg.solve(Q[:, 6:, 6:], Q[:, 6:, :6])
+    got = np.stack([b[:, N - 1, q] for q in range(21)], axis=-1)
+    want = np.stack([Pk[:, i, j] for i in range(6) for j in range(i, 6)], axis=-1)
+    np.testing.assert_allclose(got, want, rtol=1e-8, atol=1e-8 * np.abs(want).max())
