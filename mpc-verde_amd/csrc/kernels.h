@@ -293,7 +293,8 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   constexpr int kWsH = RestoWs::slots(NX, NU);  // slot-major slots before the records
   constexpr int kCS = chain_ws_slots(NX, NU);   // record: stage Hessian (NH), Sigma (NZ), A (NX^2), B (NX NU)
   constexpr int kRH = 0, kRS = NH, kRA = NH + NZ, kRB = NH + NZ + NX * NX, kRP = kRB + NX * NU;
-  static_assert(!kWsStash || (kRP + (NX + 1) * NX == kCS && kCS % 2 == 0), "chain stash record");
+  constexpr int kRZ = kRP + (NX + 1) * NX;  // the iterate across the row chain (stash below)
+  static_assert(!kWsStash || (kRZ + 5 * NZ + NX == kCS && kCS % 2 == 0), "chain stash record");
   // this thread's record (16-byte aligned: hipMalloc base, 64-thread-multiple stride, even kCS);
   // opaque, so no address is hoisted out of the solve loop
   auto wsrec = [&]() __attribute__((always_inline)) -> const double* {
@@ -1173,13 +1174,15 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
       // Stash: the iterate, its bound multipliers, bounds and lam are live across the sequential
       // chain but unused in it; for the 6-state model they go to the LDS value cache (idle
       // between evaluations) so the chain's operands keep registers instead of scratch
-      constexpr bool kStash = !Model::kParallelRiccati && NX >= 6 && Model::kTrigSlots >= 5 * NZ + NX && !kRow6;
+      // (the 6-state row chain's ring occupies that cache: the iterate waits in the workspace record)
+      constexpr bool kStash = !Model::kParallelRiccati && NX >= 6 && Model::kTrigSlots >= 5 * NZ + NX;
       auto stash = [&](bool back) __attribute__((always_inline)) {
         if constexpr (kStash) {
-          double* t = tcache + threadIdx.x;
+          double* t = kRow6 ? const_cast<double*>(wsrec()) + kRZ : tcache + threadIdx.x;
+          constexpr int st = kRow6 ? 1 : kSBS;
           auto mv = [&](double& v, int o) __attribute__((always_inline)) {
-            if (back) v = t[o * kSBS];
-            else t[o * kSBS] = v;
+            if (back) v = kRow6 ? wsload(t, o) : t[o * st];
+            else t[o * st] = v;
           };
 #pragma unroll
           for (int i = 0; i < NZ; ++i) {
@@ -1398,8 +1401,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
           // workspace stash) into the LDS ring window by window, every row runs the instance's
           // recursion and stores each node's value function into that node's workspace slots, and
           // node lane k redoes its own step from node k+1's -- the chain's step k, the same
-          // operations as riccati_step, so the same bits -- for its factors and P_k.  Without the
-          // sequential chain's early stop: a failed step still fails the attempt (fac_ok below)
+          // operations as riccati_step, so the same bits -- for its factors and P_k
           static_assert(!kDec && kWsStash, "6-state row chain: plain sequential recursion, workspace stash");
           auto fill = [&](int lo, int hi, bool top) __attribute__((always_inline)) {
             if (seq && hasU && k >= lo && k <= hi) {
@@ -1417,10 +1419,14 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
           };
           double* out0 = a.ws + (long)kWsH * a.ws_stride + (gid - k) * kCS + kRP;  // node 0's slots
           STAMP_SUB(11);
-          rowchain6::run(tcache, out0, kCS, valid && seq, N, fill);
+          const bool early = rowchain6::run(tcache, out0, kCS, valid && seq, N, fill);
           __syncthreads();  // row 0's workspace stores, before the node lanes read them
           STAMP_SUB(12);
-          if (seq) {
+          if (early) {
+            // a step's reduced Huu' failed the inertia test (the chain stopped there): the attempt
+            // fails whatever the other steps give -- the same decision as fac_ok after the full chain
+            okl = false;
+          } else if (seq) {
             if (hasU) {
               double Pin_[NP], pin_[NX], Hj[NH], Aj[NX * NX], Bj[NX * NU];
               rowchain6::load_next(wsrec() + kCS + kRP, Pin_, pin_);

@@ -194,7 +194,7 @@ __device__ __forceinline__ void run(const double* rec, int N) {
         "s_or_b64 exec, exec, %0"
         : "=&s"(saved)
         : "s"(wmask), "v"(a), "v"(o.s0), "v"(o.s1), "v"(o.s2)
-        : "memory");
+        : "memory", "scc");  // (the exec save / restore sets SCC)
   };
   // one step on the loaded stage `st`, issuing the loads of the next step (record j - 1; at j = 0 a
   // harmless re-read of record 0) into `nx` after stage 1, so their latency hides behind the step

@@ -130,8 +130,11 @@ __device__ __forceinline__ void load_next(const double* o, double* P, double* p)
 // Each group of DPP FMAs is one asm statement whose DPP sources are LDS loads or were written at
 // least two VALU instructions earlier (the VALU-write -> DPP-read hazard the compiler does not
 // see inside the asm).
+// Returns true when the chain stopped early: a step whose reduced Huu' is not positive definite
+// (fac_ok of its factors false) decides the inertia-correction attempt, so the chain ends there (every
+// lane holds the step's reciprocals; the four rows agree: a wave-uniform exit).
 template <class Fill>
-__device__ __forceinline__ void run(double* ring, double* out0, long ostride, bool writer, int N, Fill&& fill) {
+__device__ __forceinline__ bool run(double* ring, double* out0, long ostride, bool writer, int N, Fill&& fill) {
   typedef double v2d __attribute__((ext_vector_type(2)));
   // lane constants, derived inside the solve loop (opaque to loop-invariant code motion)
   int r = (int)(threadIdx.x & 15);
@@ -169,7 +172,8 @@ __device__ __forceinline__ void run(double* ring, double* out0, long ostride, bo
         "global_store_dwordx2 %2, %8, off offset:40\n\t"
         "s_or_b64 exec, exec, %0"
         : "=&s"(saved)
-        : "s"(wmask), "v"(o.o), "v"(o.s[0]), "v"(o.s[1]), "v"(o.s[2]), "v"(o.s[3]), "v"(o.s[4]), "v"(o.s[5]));
+        : "s"(wmask), "v"(o.o), "v"(o.s[0]), "v"(o.s[1]), "v"(o.s[2]), "v"(o.s[3]), "v"(o.s[4]), "v"(o.s[5])
+        : "scc");  // (the exec save / restore sets SCC)
   };
 
   int lo = N > kWin ? N - kWin : 0, hi = N - 1;
@@ -333,6 +337,9 @@ __device__ __forceinline__ void run(double* ring, double* out0, long ostride, bo
           : "v"(r0), "v"(r1), "v"(U0), "v"(t), "v"(U1));
       S0 = Q0, S1 = Q1, S2 = Q2, S3 = Q3, S4 = Q4, S5 = Q5;
       out = Out{op + (long)j * ostride, {S0, S1, S2, S3, S4, S5}};
+      // fac_ok of this step (riccati.h): pivots 1/d0 and d0/det positive and finite
+      const bool okj = r0 > 0.0 && r0 < INFINITY && r1 > 0.0 && r1 < INFINITY;
+      if (!__builtin_amdgcn_readfirstlane((int)okj)) return true;
     }
     if (lo == 0) break;
     hi = lo - 1;
@@ -345,6 +352,7 @@ __device__ __forceinline__ void run(double* ring, double* out0, long ostride, bo
     st = load(hi - lo);
   }
   store(out);  // node 0's
+  return false;
 }
 
 }  // namespace rowchain6

@@ -134,9 +134,10 @@ struct RestoWs {
 };
 // workspace chain stash of the models with kWsStash (the 6-state bicycle, model 4): the stage
 // Hessian (packed), Sigma, A and B of every lane, after the restoration slots, then the row chain's
-// value function of the lane's node (rowchain6.h: P's columns and p, (nx + 1) nx doubles)
+// value function of the lane's node (rowchain6.h: P's columns and p, (nx + 1) nx doubles) and the
+// iterate across the chain (z, zL, zU, bounds, lam)
 __host__ __device__ constexpr int chain_ws_slots(int nx, int nu) {
-  return (nx + nu) * (nx + nu + 1) / 2 + nx + nu + nx * nx + nx * nu + (nx + 1) * nx;
+  return (nx + nu) * (nx + nu + 1) / 2 + nx + nu + nx * nx + nx * nu + (nx + 1) * nx + 5 * (nx + nu) + nx;
 }
 // doubles of workspace per thread (restoration + chain stash; 0: the model uses none)
 int resto_ws_slots(int model, int nx, int nu);

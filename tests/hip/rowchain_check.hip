@@ -122,7 +122,8 @@ __device__ void put_out6(double* o, const double* P, const double* p, const Fac<
 }
 
 __global__ __launch_bounds__(64) void rowchain6_check_kernel(int N, double delta, const double* in, double* ws,
-                                                             double* out_seq, double* out_row, unsigned long long* cyc) {
+                                                             double* out_seq, double* out_row, unsigned long long* cyc,
+                                                             int* early_out) {
   namespace rc = rowchain6;
   constexpr unsigned long long AM = rc::amask6(), BM = (1ull << 12) - 1;
   __shared__ double ring[rc::kRing];
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(64) void rowchain6_check_kernel(int N, double delta
   };
   double* out0 = ws + inst * 64 * rc::kOut;
   const unsigned long long t2 = clk();
-  rc::run(ring, out0, rc::kOut, true, N, fill);
+  const bool early = rc::run(ring, out0, rc::kOut, true, N, fill);
   const unsigned long long t3 = clk();
   __syncthreads();
   double P2[21], p2[6];
@@ -180,6 +181,7 @@ __global__ __launch_bounds__(64) void rowchain6_check_kernel(int N, double delta
     }
   }
   if (k <= N) put_out6(out_row + (inst * 64 + k) * kOut6, P2, p2, fac2);
+  if (k == 0) early_out[inst] = early ? 1 : 0;  // the chain stopped at a step failing the inertia test
   if (cyc && k == 0) {
     cyc[2 * blockIdx.x] = t1 - t0;
     cyc[2 * blockIdx.x + 1] = t3 - t2;
@@ -189,11 +191,13 @@ __global__ __launch_bounds__(64) void rowchain6_check_kernel(int N, double delta
 }  // namespace mpcx
 
 // in: B * 64 * 106 doubles (node records, nodes 0..N used); ws: B * 64 * kOut scratch; outputs
-// B * 64 * 44 doubles each; cyc (may be null): per wave the cycles of the two chains
+// B * 64 * 44 doubles each; cyc (may be null): per wave the cycles of the two chains; early: per
+// instance 1 if the chain stopped at a failed inertia test
 extern "C" int rowchain6_check(int N, int B, double delta, const double* in, double* ws, double* out_seq,
-                               double* out_row, unsigned long long* cyc) {
+                               double* out_row, unsigned long long* cyc, int* early) {
   if (B <= 0 || N < 1 || N > 63) return 1;
-  hipLaunchKernelGGL(mpcx::rowchain6_check_kernel, dim3(B), dim3(64), 0, 0, N, delta, in, ws, out_seq, out_row, cyc);
+  hipLaunchKernelGGL(mpcx::rowchain6_check_kernel, dim3(B), dim3(64), 0, 0, N, delta, in, ws, out_seq, out_row, cyc,
+                     early);
   return hipDeviceSynchronize() == hipSuccess ? 0 : 3;
 }
 

@@ -95,14 +95,15 @@ K_IN6, K_OUT6, K_WS6 = 106, 44, 42
 IU8 = [(i, j) for i in range(8) for j in range(i, 8)]
 
 
-def stages6(rng, B, delta):
+def stages6(rng, B, indefinite):
     """Random 6-state stages with the model's Jacobian structure (columns x0, x1 of A unit
-    vectors, the rest dense; B dense), symmetric stage Hessians (every 7th stage with an
-    indefinite control block), Sigma, gradients and defects at all 64 nodes."""
+    vectors, the rest dense; B dense), symmetric stage Hessians (with `indefinite`, every 7th stage
+    from node 3 with an indefinite control block), Sigma, gradients and defects at all 64 nodes."""
     x = np.zeros((B, 64, K_IN6))
     Hf = rng.standard_normal((B, 64, 8, 8)) * 0.5
     Hf = Hf @ np.swapaxes(Hf, -1, -2) + np.eye(8) * rng.uniform(0.0, 2.0, (B, 64, 1, 1))
-    Hf[:, 3::7, 6:, 6:] -= 6.0 * np.eye(2)
+    if indefinite:
+        Hf[:, 3::7, 6:, 6:] -= 6.0 * np.eye(2)
     x[..., 0:36] = np.stack([Hf[..., i, j] for i, j in IU8], axis=-1)
     x[..., 36:44] = rng.uniform(0.0, 1.0, (B, 64, 8))
     A = np.eye(6) + rng.standard_normal((B, 64, 6, 6)) * 0.2
@@ -115,31 +116,47 @@ def stages6(rng, B, delta):
     return x
 
 
-@pytest.mark.parametrize("N,delta", [(50, 0.0), (50, 1e-4), (35, 0.0), (36, 0.0), (63, 0.0), (1, 0.0), (12, 3e-3)])
-def test_row_chain6_is_the_sequential_recursion(N, delta):
+@pytest.mark.parametrize("N,delta,indef", [(50, 0.0, False), (50, 1e-4, False), (35, 0.0, False), (36, 0.0, False),
+                                           (63, 0.0, False), (1, 0.0, False), (12, 3e-3, False), (50, 0.0, True),
+                                           (20, 1e-4, True)])
+def test_row_chain6_is_the_sequential_recursion(N, delta, indef):
+    """Bit for bit the sequential recursion at every node; with indefinite stages the chain stops at
+    the first step (from N - 1 down) whose factors fail the inertia test, exactly where the
+    sequential recursion's verdict first fails, and nodes at and above it still match."""
     import torch
 
     if not os.path.exists(LIB):
         pytest.fail(f"{LIB} not built (make -C tests/hip)")
     lib = ctypes.CDLL(LIB)
-    lib.rowchain6_check.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double] + [ctypes.c_void_p] * 5
+    lib.rowchain6_check.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double] + [ctypes.c_void_p] * 6
     B = 96
     rng = np.random.default_rng(7 * N + 1)
-    x = stages6(rng, B, delta)
+    x = stages6(rng, B, indef)
     d_in = torch.from_numpy(np.ascontiguousarray(x)).cuda()
     ws = torch.full((B, 64, K_WS6), np.nan, dtype=torch.float64, device="cuda")
     o_seq = torch.full((B, 64, K_OUT6), np.nan, dtype=torch.float64, device="cuda")
     o_row = torch.full_like(o_seq, np.nan)
     cyc = torch.zeros(2 * B, dtype=torch.int64, device="cuda")
+    early = torch.full((B,), -1, dtype=torch.int32, device="cuda")
     ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    assert lib.rowchain6_check(N, B, delta, ptr(d_in), ptr(ws), ptr(o_seq), ptr(o_row), ptr(cyc)) == 0
+    assert lib.rowchain6_check(N, B, delta, ptr(d_in), ptr(ws), ptr(o_seq), ptr(o_row), ptr(cyc), ptr(early)) == 0
     c = cyc.cpu().numpy().reshape(B, 2)
     print(f"N={N}: cycles per step, sequential recursion {c[:, 0].mean() / N:.0f}, row chain {c[:, 1].mean() / N:.0f}")
     a, b = o_seq.cpu().numpy()[:, :N + 1], o_row.cpu().numpy()[:, :N + 1]
-    assert np.isfinite(a[:, :N, :27]).mean() > 0.5
-    np.testing.assert_array_equal(b.view(np.int64), a.view(np.int64))
-    # a Riccati recursion: node N-1's P_{N-1} from the formula (a stage with a definite control block)
-    if (N - 1) % 7 == 3:
+    r0, r1 = a[:, :N, 27], a[:, :N, 29]
+    with np.errstate(invalid="ignore"):
+        bad = ~((r0 > 0) & (r0 < np.inf) & (r1 > 0) & (r1 < np.inf))  # fac_ok false, node by node
+    first = np.where(bad.any(axis=1), N - 1 - np.argmax(bad[:, ::-1], axis=1), -1)  # first failure from N - 1 down
+    np.testing.assert_array_equal(early.cpu().numpy(), (first >= 0).astype(np.int32))
+    if indef:
+        assert (first >= 0).mean() > 0.5
+    else:
+        assert (first < 0).all()
+    for i in range(B):  # nodes the chain reached (all of them when it ran to node 0)
+        lo = max(first[i], 0)
+        np.testing.assert_array_equal(b[i, lo:].view(np.int64), a[i, lo:].view(np.int64))
+    # a Riccati recursion: node N-1's P_{N-1} from the formula
+    if indef:
         return
     s = x[:, N - 1]
     Hf = np.zeros((B, 8, 8))
