@@ -2465,7 +2465,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
       }
     }
     if (!done && !accepted && !handled) {
-#ifdef MPCX_STAMPS
+#ifdef MPCX_DEBUG_PRINT  // (not in the stamps build: its ISA is the product's, phase by phase)
       if (k == 0)
         printf("LSFAIL inst=%d step=%d it=%d mu=%.3e thk=%.6e phk=%.10e gd=%.3e amax=%.3e alpha=%.3e amin=%.3e "
                "node-0 Ed=%.3e Ec=%.3e Ecomp=%.3e E0=%.3e fs=%.3e dw=%.1e\n",

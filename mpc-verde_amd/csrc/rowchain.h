@@ -197,8 +197,11 @@ __device__ __forceinline__ void run(const double* rec, int N) {
         : "memory", "scc");  // (the exec save / restore sets SCC)
   };
   // one step on the loaded stage `st`, issuing the loads of the next step (record j - 1; at j = 0 a
-  // harmless re-read of record 0) into `nx` after stage 1, so their latency hides behind the step
-  auto step = [&](auto prev, int j, Stage& st, Out& out) __attribute__((always_inline)) {
+  // harmless re-read of record 0) into `nx` after stage 2, so their latency hides behind the step;
+  // the previous step's results `po` go out, this step's are `no`.  Two stage and two result
+  // variables alternate between consecutive steps (the loop below is unrolled by two): a single
+  // loop-carried set would cost register copies at every back edge
+  auto step = [&](auto prev, int j, const Stage& st, Stage& nx, const Out& po, Out& no) __attribute__((always_inline)) {
     double* rj = base + j * kRec;
     const double H0 = st.L0.x, H1 = st.L0.y, H2 = st.L1.x, H3 = st.L1.y, H4 = st.L2.x;
     const double cf0 = st.L2.y, cf1 = st.L3.x, cf2 = st.L3.y;
@@ -254,8 +257,9 @@ __device__ __forceinline__ void run(const double* rec, int N) {
     // the previous step's results go out first: behind this step's stage 2, well before the next
     // step waits for its loads (LDS operations complete in order, so that wait covers the stores too)
     if constexpr (decltype(prev)::value)
-      if (!(MPCX_ROWCHAIN_PROBE & 1)) store(out);
-    if (!(MPCX_ROWCHAIN_PROBE & 2)) st = load(j > 0 ? j - 1 : 0);
+      if (!(MPCX_ROWCHAIN_PROBE & 1)) store(po);
+    if (!(MPCX_ROWCHAIN_PROBE & 2)) nx = load(j > 0 ? j - 1 : 0);
+    else nx = st;
     __builtin_amdgcn_sched_barrier(0);
     // lane s: g0 = gu0, and gu1 for g1 (stage 2's u0 / u1 sums there)
     const double h0c = on_s ? Q3 : hq0;
@@ -286,13 +290,18 @@ __device__ __forceinline__ void run(const double* rec, int N) {
         : "v"(r0), "v"(r1), "v"(h0c), "v"(t), "v"(hu1c));
     // ---- node j's results, stored during the next step (every lane writes its own block; only the
     // columns read back matter)
-    out = Out{rj, S0, S1, S2};  // stored during the next step
+    no = Out{rj, S0, S1, S2};  // stored during the next step
   };
-  Stage st = load(N - 1);
-  Out out{};
-  step(std::false_type{}, N - 1, st, out);
-  for (int j = N - 2; j >= 0; --j) step(std::true_type{}, j, st, out);
-  if (!(MPCX_ROWCHAIN_PROBE & 1)) store(out);  // step 0's results
+  Stage sa = load(N - 1), sb;
+  Out oa{}, ob{};
+  step(std::false_type{}, N - 1, sa, sb, oa, ob);
+  int j = N - 2;
+  for (; j >= 1; j -= 2) {
+    step(std::true_type{}, j, sb, sa, ob, oa);
+    step(std::true_type{}, j - 1, sa, sb, oa, ob);
+  }
+  if (j == 0) step(std::true_type{}, 0, sb, sa, ob, oa);
+  if (!(MPCX_ROWCHAIN_PROBE & 1)) store(j == 0 ? oa : ob);  // step 0's results
 }
 
 }  // namespace rowchain

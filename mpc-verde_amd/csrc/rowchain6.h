@@ -185,161 +185,174 @@ __device__ __forceinline__ bool run(double* ring, double* out0, long ostride, bo
     const double* t = bp + (N - lo) * kRec;
     S0 = t[0], S1 = t[1], S2 = t[2], S3 = t[3], S4 = t[4], S5 = t[5];
   }
-  Out out{op + (long)N * ostride, {S0, S1, S2, S3, S4, S5}};  // node N's (stored during step N - 1)
-  Stage st = load(hi - lo);
+  Out oa{op + (long)N * ostride, {S0, S1, S2, S3, S4, S5}}, ob;  // node N's (stored during step N - 1)
+  // one step on the loaded stage `st`, the next record's loads into `nx`, the previous step's
+  // results `po` stored and this step's in `no`; true = the step fails the inertia test.  Two stage
+  // and two result variables alternate between steps (pairs of steps below): one loop-carried set
+  // would cost register copies at every back edge
+  auto step = [&](int j, const Stage& st, Stage& nx, const Out& po, Out& no) __attribute__((always_inline)) {
+    const double H0 = st.L[0].x, H1 = st.L[0].y, H2 = st.L[1].x, H3 = st.L[1].y, H4 = st.L[2].x,
+                 H5 = st.L[2].y;
+    const double W0 = st.L[4].x, W1 = st.L[4].y, W2 = st.L[5].x, W3 = st.L[5].y, W4 = st.L[6].x,
+                 W5 = st.L[6].y;
+    // ---- stage 1: V_r = sum_m P_{rm} w_m (p_r first on lane s).  The six start values V = S m_s
+    // only READ the DPP sources S, and put any earlier VALU write of S two instructions back
+    double V0, V1, V2, V3, V4, V5;
+    asm volatile(
+        "v_mul_f64 %0, %6, %18\n\t"
+        "v_mul_f64 %1, %7, %18\n\t"
+        "v_mul_f64 %2, %8, %18\n\t"
+        "v_mul_f64 %3, %9, %18\n\t"
+        "v_mul_f64 %4, %10, %18\n\t"
+        "v_mul_f64 %5, %11, %18\n\t"
+        "v_fmac_f64_dpp %0, %6, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %6, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %6, %12 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %6, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %6, %12 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %6, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %6, %13 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %7, %13 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %7, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %7, %13 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %7, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %7, %13 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %6, %14 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %7, %14 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %8, %14 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %8, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %8, %14 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %8, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %6, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %7, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %8, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %9, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %9, %15 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %9, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %6, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %7, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %8, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %9, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %10, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %10, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %6, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %7, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %8, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %9, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %10, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %11, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf"
+        : "=&v"(V0), "=&v"(V1), "=&v"(V2), "=&v"(V3), "=&v"(V4), "=&v"(V5)
+        : "v"(S0), "v"(S1), "v"(S2), "v"(S3), "v"(S4), "v"(S5), "v"(W0), "v"(W1), "v"(W2), "v"(W3), "v"(W4),
+          "v"(W5), "v"(m_s));
+    // ---- stage 2: x rows (A's columns x0, x1: their one entry), then the u rows on the s and u
+    // lanes (bank 2) and the A^T (P B) sums on the x lanes (banks 0-1) into the same accumulators.
+    // The s_nop covers a register copy of a W the compiler might place just before the block.
+    double Q0 = H0, Q1 = H1, Q2 = H2, Q3 = H3, Q4 = H4, Q5 = H5, U0 = st.L[3].x, U1 = st.L[3].y;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %14, %8 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %15, %9 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %14, %8 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %8 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %14, %8 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %14, %8 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %7, %14, %8 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %2, %15, %9 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %15, %9 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %9 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %15, %9 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %9 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %7, %15, %9 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %2, %16, %10 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %16, %10 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %16, %10 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %10 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %16, %10 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %7, %16, %10 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %2, %17, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %17, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %17, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %17, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %17, %11 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %7, %17, %11 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %2, %18, %12 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %18, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %18, %12 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %18, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %18, %12 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %7, %18, %12 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %2, %19, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %19, %13 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %19, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %19, %13 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %19, %13 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %7, %19, %13 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
+        "v_fmac_f64_dpp %6, %8, %14 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
+        "v_fmac_f64_dpp %7, %8, %14 row_newbcast:10 row_mask:0xf bank_mask:0x3\n\t"
+        "v_fmac_f64_dpp %6, %9, %15 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
+        "v_fmac_f64_dpp %7, %9, %15 row_newbcast:10 row_mask:0xf bank_mask:0x3\n\t"
+        "v_fmac_f64_dpp %6, %10, %16 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
+        "v_fmac_f64_dpp %7, %10, %16 row_newbcast:10 row_mask:0xf bank_mask:0x3\n\t"
+        "v_fmac_f64_dpp %6, %11, %17 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
+        "v_fmac_f64_dpp %7, %11, %17 row_newbcast:10 row_mask:0xf bank_mask:0x3\n\t"
+        "v_fmac_f64_dpp %6, %12, %18 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
+        "v_fmac_f64_dpp %7, %12, %18 row_newbcast:10 row_mask:0xf bank_mask:0x3\n\t"
+        "v_fmac_f64_dpp %6, %13, %19 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
+        "v_fmac_f64_dpp %7, %13, %19 row_newbcast:10 row_mask:0xf bank_mask:0x3"
+        : "+v"(Q0), "+v"(Q1), "+v"(Q2), "+v"(Q3), "+v"(Q4), "+v"(Q5), "+v"(U0), "+v"(U1)
+        : "v"(V0), "v"(V1), "v"(V2), "v"(V3), "v"(V4), "v"(V5), "v"(W0), "v"(W1), "v"(W2), "v"(W3), "v"(W4),
+          "v"(W5));
+    // the stage data are consumed: the previous step's value function goes out, the next step's
+    // record (slot j - 1 - lo; at j = lo a harmless re-read) loads behind the factor and update
+    __builtin_amdgcn_sched_barrier(0);
+    store(po);
+    nx = load(j > lo ? j - 1 - lo : 0);
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- factor: Huu' = [[a, b], [b, d]] (a on lane u0, b and d on lane u1), every lane
+    const double fa = rowchain::bcast<kLU0>(U0), fb = rowchain::bcast<kLU1>(U0), fd = rowchain::bcast<kLU1>(U1);
+    const double det = fma(fa, fd, -fb * fb);
+    const double r0 = rcp64(fa), rdet = rcp64(det);
+    const double t = fb * r0;
+    const double r1 = fa * rdet;
+    // ---- update: P_k(i, c) = Hxx'(i, c) - (r0 h0_i) h0_c - (r1 h1_i) h1_c, (r h)_i from lane x_i;
+    // h0_c = U0 (lane s: gu0), h1_c = U1 - t U0.  R0 is written two VALU instructions before its
+    // first DPP read, R1 six
+    double R0, R1, h1c;
+    asm volatile(
+        "v_mul_f64 %7, %9, %11\n\t"
+        "v_fma_f64 %6, -%12, %11, %13\n\t"
+        "v_mul_f64 %8, %10, %6\n\t"
+        "v_fmac_f64_dpp %0, -%7, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, -%7, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, -%7, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, -%7, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, -%7, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, -%7, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, -%8, %6 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, -%8, %6 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, -%8, %6 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, -%8, %6 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, -%8, %6 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, -%8, %6 row_newbcast:5 row_mask:0xf bank_mask:0xf"
+        : "+v"(Q0), "+v"(Q1), "+v"(Q2), "+v"(Q3), "+v"(Q4), "+v"(Q5), "=&v"(h1c), "=&v"(R0), "=&v"(R1)
+        : "v"(r0), "v"(r1), "v"(U0), "v"(t), "v"(U1));
+    S0 = Q0, S1 = Q1, S2 = Q2, S3 = Q3, S4 = Q4, S5 = Q5;
+    no = Out{op + (long)j * ostride, {S0, S1, S2, S3, S4, S5}};
+    // fac_ok of this step (riccati.h): pivots 1/d0 and d0/det positive and finite
+    const bool okj = r0 > 0.0 && r0 < INFINITY && r1 > 0.0 && r1 < INFINITY;
+    return !__builtin_amdgcn_readfirstlane((int)okj);
+  };
+  Stage sa = load(hi - lo), sb;
   for (;;) {
-    for (int j = hi; j >= lo; --j) {
-      const double H0 = st.L[0].x, H1 = st.L[0].y, H2 = st.L[1].x, H3 = st.L[1].y, H4 = st.L[2].x,
-                   H5 = st.L[2].y;
-      const double W0 = st.L[4].x, W1 = st.L[4].y, W2 = st.L[5].x, W3 = st.L[5].y, W4 = st.L[6].x,
-                   W5 = st.L[6].y;
-      // ---- stage 1: V_r = sum_m P_{rm} w_m (p_r first on lane s).  The six start values V = S m_s
-      // only READ the DPP sources S, and put any earlier VALU write of S two instructions back
-      double V0, V1, V2, V3, V4, V5;
-      asm volatile(
-          "v_mul_f64 %0, %6, %18\n\t"
-          "v_mul_f64 %1, %7, %18\n\t"
-          "v_mul_f64 %2, %8, %18\n\t"
-          "v_mul_f64 %3, %9, %18\n\t"
-          "v_mul_f64 %4, %10, %18\n\t"
-          "v_mul_f64 %5, %11, %18\n\t"
-          "v_fmac_f64_dpp %0, %6, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %1, %6, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %2, %6, %12 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %6, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %6, %12 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %6, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %0, %6, %13 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %1, %7, %13 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %2, %7, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %7, %13 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %7, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %7, %13 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %0, %6, %14 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %1, %7, %14 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %2, %8, %14 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %8, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %8, %14 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %8, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %0, %6, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %1, %7, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %2, %8, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %9, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %9, %15 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %9, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %0, %6, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %1, %7, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %2, %8, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %9, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %10, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %10, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %0, %6, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %1, %7, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %2, %8, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %9, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %10, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %11, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf"
-          : "=&v"(V0), "=&v"(V1), "=&v"(V2), "=&v"(V3), "=&v"(V4), "=&v"(V5)
-          : "v"(S0), "v"(S1), "v"(S2), "v"(S3), "v"(S4), "v"(S5), "v"(W0), "v"(W1), "v"(W2), "v"(W3), "v"(W4),
-            "v"(W5), "v"(m_s));
-      // ---- stage 2: x rows (A's columns x0, x1: their one entry), then the u rows on the s and u
-      // lanes (bank 2) and the A^T (P B) sums on the x lanes (banks 0-1) into the same accumulators.
-      // The s_nop covers a register copy of a W the compiler might place just before the block.
-      double Q0 = H0, Q1 = H1, Q2 = H2, Q3 = H3, Q4 = H4, Q5 = H5, U0 = st.L[3].x, U1 = st.L[3].y;
-      asm volatile(
-          "s_nop 1\n\t"
-          "v_fmac_f64_dpp %0, %14, %8 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %1, %15, %9 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %2, %14, %8 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %14, %8 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %14, %8 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %14, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %6, %14, %8 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %7, %14, %8 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %2, %15, %9 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %15, %9 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %15, %9 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %15, %9 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %6, %15, %9 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %7, %15, %9 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %2, %16, %10 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %16, %10 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %16, %10 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %16, %10 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %6, %16, %10 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %7, %16, %10 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %2, %17, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %17, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %17, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %17, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %6, %17, %11 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %7, %17, %11 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %2, %18, %12 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %18, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %18, %12 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %18, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %6, %18, %12 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %7, %18, %12 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %2, %19, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, %19, %13 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, %19, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, %19, %13 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %6, %19, %13 row_newbcast:9 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %7, %19, %13 row_newbcast:10 row_mask:0xf bank_mask:0x4\n\t"
-          "v_fmac_f64_dpp %6, %8, %14 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
-          "v_fmac_f64_dpp %7, %8, %14 row_newbcast:10 row_mask:0xf bank_mask:0x3\n\t"
-          "v_fmac_f64_dpp %6, %9, %15 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
-          "v_fmac_f64_dpp %7, %9, %15 row_newbcast:10 row_mask:0xf bank_mask:0x3\n\t"
-          "v_fmac_f64_dpp %6, %10, %16 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
-          "v_fmac_f64_dpp %7, %10, %16 row_newbcast:10 row_mask:0xf bank_mask:0x3\n\t"
-          "v_fmac_f64_dpp %6, %11, %17 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
-          "v_fmac_f64_dpp %7, %11, %17 row_newbcast:10 row_mask:0xf bank_mask:0x3\n\t"
-          "v_fmac_f64_dpp %6, %12, %18 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
-          "v_fmac_f64_dpp %7, %12, %18 row_newbcast:10 row_mask:0xf bank_mask:0x3\n\t"
-          "v_fmac_f64_dpp %6, %13, %19 row_newbcast:9 row_mask:0xf bank_mask:0x3\n\t"
-          "v_fmac_f64_dpp %7, %13, %19 row_newbcast:10 row_mask:0xf bank_mask:0x3"
-          : "+v"(Q0), "+v"(Q1), "+v"(Q2), "+v"(Q3), "+v"(Q4), "+v"(Q5), "+v"(U0), "+v"(U1)
-          : "v"(V0), "v"(V1), "v"(V2), "v"(V3), "v"(V4), "v"(V5), "v"(W0), "v"(W1), "v"(W2), "v"(W3), "v"(W4),
-            "v"(W5));
-      // the stage data are consumed: the previous step's value function goes out, the next step's
-      // record (slot j - 1 - lo; at j = lo a harmless re-read) loads behind the factor and update
-      __builtin_amdgcn_sched_barrier(0);
-      store(out);
-      st = load(j > lo ? j - 1 - lo : 0);
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- factor: Huu' = [[a, b], [b, d]] (a on lane u0, b and d on lane u1), every lane
-      const double fa = rowchain::bcast<kLU0>(U0), fb = rowchain::bcast<kLU1>(U0), fd = rowchain::bcast<kLU1>(U1);
-      const double det = fma(fa, fd, -fb * fb);
-      const double r0 = rcp64(fa), rdet = rcp64(det);
-      const double t = fb * r0;
-      const double r1 = fa * rdet;
-      // ---- update: P_k(i, c) = Hxx'(i, c) - (r0 h0_i) h0_c - (r1 h1_i) h1_c, (r h)_i from lane x_i;
-      // h0_c = U0 (lane s: gu0), h1_c = U1 - t U0.  R0 is written two VALU instructions before its
-      // first DPP read, R1 six
-      double R0, R1, h1c;
-      asm volatile(
-          "v_mul_f64 %7, %9, %11\n\t"
-          "v_fma_f64 %6, -%12, %11, %13\n\t"
-          "v_mul_f64 %8, %10, %6\n\t"
-          "v_fmac_f64_dpp %0, -%7, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %1, -%7, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %2, -%7, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, -%7, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, -%7, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, -%7, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %0, -%8, %6 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %1, -%8, %6 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %2, -%8, %6 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %3, -%8, %6 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %4, -%8, %6 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-          "v_fmac_f64_dpp %5, -%8, %6 row_newbcast:5 row_mask:0xf bank_mask:0xf"
-          : "+v"(Q0), "+v"(Q1), "+v"(Q2), "+v"(Q3), "+v"(Q4), "+v"(Q5), "=&v"(h1c), "=&v"(R0), "=&v"(R1)
-          : "v"(r0), "v"(r1), "v"(U0), "v"(t), "v"(U1));
-      S0 = Q0, S1 = Q1, S2 = Q2, S3 = Q3, S4 = Q4, S5 = Q5;
-      out = Out{op + (long)j * ostride, {S0, S1, S2, S3, S4, S5}};
-      // fac_ok of this step (riccati.h): pivots 1/d0 and d0/det positive and finite
-      const bool okj = r0 > 0.0 && r0 < INFINITY && r1 > 0.0 && r1 < INFINITY;
-      if (!__builtin_amdgcn_readfirstlane((int)okj)) return true;
+    int j = hi;
+    for (; j > lo; j -= 2) {
+      if (step(j, sa, sb, oa, ob)) return true;
+      if (step(j - 1, sb, sa, ob, oa)) return true;
+    }
+    if (j == lo) {
+      if (step(lo, sa, sb, oa, ob)) return true;
+      oa = ob;
     }
     if (lo == 0) break;
     hi = lo - 1;
@@ -349,9 +362,9 @@ __device__ __forceinline__ bool run(double* ring, double* out0, long ostride, bo
     asm volatile("" ::: "memory");
     fill(lo, hi, false);
     asm volatile("" ::: "memory");
-    st = load(hi - lo);
+    sa = load(hi - lo);
   }
-  store(out);  // node 0's
+  store(oa);  // node 0's
   return false;
 }
 
