@@ -96,13 +96,16 @@ def budget(blocks, trips):
             tgt = cur["straight"] if key == "straight" else cur["loops"].setdefault(f"{b['header']}@{b['depth']}", {})
             c = classify(mn)
             tgt[c] = tgt.get(c, 0) + 1
+            if mn.startswith("v_rcp_f64"):  # (counted again: the Riccati chain's steps per loop body)
+                tgt["_rcp"] = tgt.get("_rcp", 0) + 1
     out = []
     for i, p in enumerate(phases):
         dyn = dict(p["straight"])
         for name, cnt in p["loops"].items():
             t = trips.get(name.split("@")[0], 1)
             for c, n in cnt.items():
-                dyn[c] = dyn.get(c, 0) + t * n
+                if not c.startswith("_"):
+                    dyn[c] = dyn.get(c, 0) + t * n
         out.append({"region": i, "phase": p["phase"], "straight": p["straight"], "loops": p["loops"],
                     "dynamic_estimate": dyn, "valu": dyn.get("valu_f64", 0) + dyn.get("valu_other", 0)})
     return out

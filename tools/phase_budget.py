@@ -58,7 +58,8 @@ def main():
     a = ap.parse_args()
     blocks = ipb.parse(ipb.kernel_lines(a.asm, a.symbol))
     regions = ipb.budget(blocks, {})
-    # the chain loop: the innermost loop of the ric_chain regions runs N times
+    # the chain loop: the Riccati sub-phases' loop whose body holds the steps' reciprocals (two
+    # v_rcp_f64 per step: the sequential chain one step per trip, the row chains two) runs N steps
     per = {}
     for i, r in enumerate(regions):
         ph = r["phase"]
@@ -72,9 +73,10 @@ def main():
         acc = per.setdefault(name, {"valu": 0, "valu_f64": 0, "lds": 0, "vmem": 0, "salu": 0})
         parts = [(r["straight"], 1)]
         if r["loops"]:
-            deepest = max(int(k.split("@")[1]) for k in r["loops"])
             for k, cnt in r["loops"].items():
-                t = a.N if (name == "ric_chain" and int(k.split("@")[1]) == deepest) else 1
+                # (depth 3: inside the solve loop and the inertia-correction attempts)
+                steps = cnt.get("_rcp", 0) // 2 if int(k.split("@")[1]) >= 3 else 0
+                t = a.N / steps if (name in ("ric_scan", "ric_chain") and steps) else 1
                 parts.append((cnt, t))
         for cnt, t in parts:
             for c, v in cnt.items():
@@ -99,7 +101,7 @@ def main():
         "sweep": ["sweep"],
     }
     out = {"_meta": {"kernel": a.symbol, "N": a.N, "source": "static ISA of the stamps build (instructions per IPM "
-                     "iteration: chain loop x N, other loops x 1) + s_memtime stamps of the slowest wave (cycles)",
+                     "iteration: chain loop x N steps, other loops x 1) + s_memtime stamps of the slowest wave (cycles)",
                      "cycles_per_iteration": round(cyc), "iters_slowest_wave": st.get("iters_slowest_wave")},
            "phases": {}}
     for g, members in groups.items():
