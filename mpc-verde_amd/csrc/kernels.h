@@ -33,7 +33,6 @@
 #include "pscan.h"
 #include "riccati.h"
 #include "rowchain.h"
-#include "rowchain5.h"
 #include "rowchain6.h"
 #include "solver.h"
 
@@ -286,10 +285,6 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
   // the row chain's node records (rowchain.h): G records per instance of the wave
   constexpr bool kRow = RowChainOf<Model>::value && rowchain::fits<Model>() && G >= 32 && G * R <= 64;
   __shared__ double rcbuf[kRow ? (64 / (G * R)) * G * rowchain::kRec : 1];
-  // the 5-state linear model's full steps after its decoupled suffix's scan (rowchain5.h): wave 0 of
-  // a multi-wave group, node records for at most rowchain5::kMax steps
-  constexpr bool kRow5 = rowchain5::fits<Model>() && DecSuffixOf<Model>::value && G > 64 && R == 1;
-  __shared__ double rc5buf[kRow5 ? (rowchain5::kMax + 1) * rowchain5::kRec : 1];
   // workspace chain stash (solver.h chain_ws_slots): slots after the restoration workspace's
   constexpr bool kWsStash = WsStashOf<Model>::value;
   // The stash is one contiguous record per thread (array of structures, after the restoration
@@ -1535,26 +1530,7 @@ __global__ __launch_bounds__(G * R > 64 ? G * R : 64) void solve_kernel(SolveArg
             if (seq) okl = !early && (!hasU || fac_ok<NX, NU>(fac));
         } else {  // wave by wave, N-side first; the value function crosses waves through LDS
           const int wv = (int)(threadIdx.x >> 6);
-          // the 5-state row chain (rowchain5.h): when the scan has taken the reused suffix, the full
-          // steps jc - 1 .. 0 are wave 0's; its node lanes write their stages, node jc its value
-          // function, the rows run the steps and each node lane reads back its own P_k, p_k, factors
-          // and verdict -- the same operations as riccati_step, so the same bits.  Block-uniform:
-          // every wave skips the wave-by-wave loop (and its exchanges) together
-          bool rowdone = false;
-          if constexpr (kRow5) {
-            if (sscan && jc >= 1 && jc <= rowchain5::kMax) {
-              rowdone = true;
-              if (wv == 0) {
-                if (seq && k < jc) rowchain5::store_node(rc5buf + k * rowchain5::kRec, Hd, gp, Aop, Bop, cdef);
-                if (seq && k == jc) rowchain5::store_terminal(rc5buf + jc * rowchain5::kRec, P, p);
-                asm volatile("" ::: "memory");  // (one wave: its LDS operations complete in order)
-                rowchain5::run(rc5buf, jc);
-                asm volatile("" ::: "memory");
-                if (seq && k < jc) okl = rowchain5::load_result(rc5buf + k * rowchain5::kRec, P, p, fac);
-              }
-            }
-          }
-          for (int ph = XWave<G>::W - 1; !rowdone && ph >= 0; --ph) {
+          for (int ph = XWave<G>::W - 1; ph >= 0; --ph) {
             if (wv == ph) {
               const double* in = xw.prev();  // (P, p) of node 64 (ph + 1), written last phase
               const int jtop = 64 * ph + 63;

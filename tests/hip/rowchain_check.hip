@@ -8,7 +8,6 @@
 // from each node's own step redone on the chain's value functions, as in the solve kernel.  Built into tests/hip/librowchain_check.so
 // (tests/hip/Makefile); used by tests/test_gpu_rowchain.py only.
 #include "kernels.h"
-#include "rowchain5.h"
 #include "rowchain6.h"
 
 namespace mpcx {
@@ -189,88 +188,7 @@ __global__ __launch_bounds__(64) void rowchain6_check_kernel(int N, double delta
   }
 }
 
-// ---- the 5-state, one-input chain (rowchain5.h): one instance per 64-lane wave, steps jc-1 .. 0 from
-// node jc's value function, riccati_step<5, 1, dense, dense, DEC = false, SREORD = true> as the
-// solve kernel's multi-wave full steps run it
-// in, per node (64 per instance): Hd 21 (packed 6x6), gp 6, A 25, B 5, c 5, P 15, p 5 (P, p used at
-// node jc only) = 82 doubles; out per node: P 15, p 5, r0, t, r1, h0 5, h1 5, g0, g1, ok = 36
-constexpr int kIn5 = 82, kOut5 = 36;
-
-__device__ void put_out5(double* o, const double* P, const double* p, const Fac<5, 1>& f, bool ok) {
-  for (int i = 0; i < 15; ++i) o[i] = P[i];
-  for (int i = 0; i < 5; ++i) o[15 + i] = p[i];
-  o[20] = f.r0;
-  o[21] = f.t;
-  o[22] = f.r1;
-  for (int i = 0; i < 5; ++i) {
-    o[23 + i] = f.h0[i];
-    o[28 + i] = f.h1[i];
-  }
-  o[33] = f.g0;
-  o[34] = f.g1;
-  o[35] = ok ? 1.0 : 0.0;
-}
-
-__global__ __launch_bounds__(64) void rowchain5_check_kernel(int jc, const double* in, double* out_seq,
-                                                             double* out_row, unsigned long long* cyc) {
-  namespace rc = rowchain5;
-  constexpr unsigned long long AM = (1ull << 25) - 1, BM = (1ull << 5) - 1;
-  __shared__ double rec[(rc::kMax + 1) * rc::kRec];
-  const int k = (int)threadIdx.x;
-  const long inst = blockIdx.x;
-  double Hd[21] = {}, gp[6] = {}, A[25] = {}, Bm[5] = {}, c[5] = {}, PT[15] = {}, pT[5] = {};
-  if (k <= jc) {
-    const double* r = in + (inst * 64 + k) * kIn5;
-    for (int i = 0; i < 21; ++i) Hd[i] = r[i];
-    for (int i = 0; i < 6; ++i) gp[i] = r[21 + i];
-    for (int i = 0; i < 25; ++i) A[i] = r[27 + i];
-    for (int i = 0; i < 5; ++i) Bm[i] = r[52 + i];
-    for (int i = 0; i < 5; ++i) c[i] = r[57 + i];
-    for (int i = 0; i < 15; ++i) PT[i] = r[62 + i];
-    for (int i = 0; i < 5; ++i) pT[i] = r[77 + i];
-  }
-  // ---- the sequential recursion
-  double P[15], p[5];
-  for (int i = 0; i < 15; ++i) P[i] = k == jc ? PT[i] : 0.0;
-  for (int i = 0; i < 5; ++i) p[i] = k == jc ? pT[i] : 0.0;
-  Fac<5, 1> fac = {};
-  bool ok = true;
-  const unsigned long long t0 = clk();
-  for (int j = jc - 1; j >= 0; --j) {
-    double Pin_[15], pin_[5];
-    for (int i = 0; i < 15; ++i) Pin_[i] = from_next(P[i]);
-    for (int i = 0; i < 5; ++i) pin_[i] = from_next(p[i]);
-    if (k == j) ok = riccati_step<5, 1, AM, BM, false, true, 0>(Hd, gp, A, Bm, c, Pin_, pin_, P, p, fac);
-  }
-  const unsigned long long t1 = clk();
-  if (k < jc) put_out5(out_seq + (inst * 64 + k) * kOut5, P, p, fac, ok);
-  // ---- the row chain
-  if (k < jc) rc::store_node(rec + k * rc::kRec, Hd, gp, A, Bm, c);
-  if (k == jc) rc::store_terminal(rec + jc * rc::kRec, PT, pT);
-  __syncthreads();
-  const unsigned long long t2 = clk();
-  rc::run(rec, jc);
-  const unsigned long long t3 = clk();
-  __syncthreads();
-  double P2[15] = {}, p2[5] = {};
-  Fac<5, 1> fac2 = {};
-  bool ok2 = true;
-  if (k < jc) ok2 = rc::load_result(rec + k * rc::kRec, P2, p2, fac2);
-  if (k < jc) put_out5(out_row + (inst * 64 + k) * kOut5, P2, p2, fac2, ok2);
-  if (cyc && k == 0) {
-    cyc[2 * blockIdx.x] = t1 - t0;
-    cyc[2 * blockIdx.x + 1] = t3 - t2;
-  }
-}
-
 }  // namespace mpcx
-
-extern "C" int rowchain5_check(int jc, int B, const double* in, double* out_seq, double* out_row,
-                               unsigned long long* cyc) {
-  if (B <= 0 || jc < 1 || jc > mpcx::rowchain5::kMax) return 1;
-  hipLaunchKernelGGL(mpcx::rowchain5_check_kernel, dim3(B), dim3(64), 0, 0, jc, in, out_seq, out_row, cyc);
-  return hipDeviceSynchronize() == hipSuccess ? 0 : 3;
-}
 
 // in: B * 64 * 106 doubles (node records, nodes 0..N used); ws: B * 64 * kOut scratch; outputs
 // B * 64 * 44 doubles each; cyc (may be null): per wave the cycles of the two chains; early: per

@@ -171,67 +171,3 @@ def test_row_chain6_is_the_sequential_recursion(N, delta, indef):
     got = np.stack([b[:, N - 1, q] for q in range(21)], axis=-1)
     want = np.stack([Pk[:, i, j] for i in range(6) for j in range(i, 6)], axis=-1)
     np.testing.assert_allclose(got, want, rtol=1e-8, atol=1e-8 * np.abs(want).max())
-
-
-# ---- rowchain5.h: config 5's full steps (5 states, one input; dense A and B with exact zeros)
-K_IN5, K_OUT5 = 82, 36
-IU6 = [(i, j) for i in range(6) for j in range(i, 6)]
-IU5 = [(i, j) for i in range(5) for j in range(i, 5)]
-
-
-def stages5(rng, B):
-    """Random stages shaped like the cart-pole QP's (u_prev augmentation: A's last row and column
-    exactly zero, B's last entry 1, exact zeros in the stage Hessian), every 5th instance with a
-    negative input curvature (an indefinite Huu'), and a terminal value function at every node."""
-    x = np.zeros((B, 64, K_IN5))
-    Hf = rng.standard_normal((B, 64, 6, 6)) * 0.5
-    Hf = Hf @ np.swapaxes(Hf, -1, -2) + np.eye(6) * rng.uniform(0.1, 2.0, (B, 64, 1, 1))
-    Hf[..., :4, 4] = Hf[..., 4, :4] = 0.0
-    Hf[..., 0, 1] = Hf[..., 1, 0] = 0.0
-    Hf[::2, :, 4, 5] = Hf[::2, :, 5, 4] = 0.0  # then P_k's last column is a signed zero off the diagonal
-    Hf[::5, :, 5, 5] -= 50.0
-    x[..., 0:21] = np.stack([Hf[..., i, j] for i, j in IU6], axis=-1)
-    x[..., 21:27] = rng.standard_normal((B, 64, 6))
-    A = np.eye(5) + rng.standard_normal((B, 64, 5, 5)) * 0.3
-    A[..., 4, :] = 0.0
-    A[..., :, 4] = 0.0
-    x[..., 27:52] = A.reshape(B, 64, 25)
-    Bm = rng.standard_normal((B, 64, 5)) * 0.3
-    Bm[..., 4] = 1.0
-    x[..., 52:57] = Bm
-    c = rng.standard_normal((B, 64, 5)) * 1e-2
-    c[..., 4] = 0.0
-    x[..., 57:62] = c
-    Pf = rng.standard_normal((B, 64, 5, 5))
-    Pf = Pf @ np.swapaxes(Pf, -1, -2) + np.eye(5)
-    x[..., 62:77] = np.stack([Pf[..., i, j] for i, j in IU5], axis=-1)
-    x[..., 77:82] = rng.standard_normal((B, 64, 5))
-    return x
-
-
-@pytest.mark.parametrize("jc", [1, 2, 5, 8])
-def test_row_chain5_is_the_sequential_recursion(jc):
-    """P_k, p_k, the factors and the step's verdict (d0 > 0) of every node, bit for bit (signs of
-    exact zeros included), against riccati_step<5, 1> with SREORD as the multi-wave kernel runs it."""
-    import torch
-
-    if not os.path.exists(LIB):
-        pytest.fail(f"{LIB} not built (make -C tests/hip)")
-    lib = ctypes.CDLL(LIB)
-    lib.rowchain5_check.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4
-    B = 128
-    rng = np.random.default_rng(100 + jc)
-    x = stages5(rng, B)
-    d_in = torch.from_numpy(np.ascontiguousarray(x)).cuda()
-    o_seq = torch.full((B, 64, K_OUT5), np.nan, dtype=torch.float64, device="cuda")
-    o_row = torch.full_like(o_seq, np.nan)
-    cyc = torch.zeros(2 * B, dtype=torch.int64, device="cuda")
-    ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    assert lib.rowchain5_check(jc, B, ptr(d_in), ptr(o_seq), ptr(o_row), ptr(cyc)) == 0
-    c = cyc.cpu().numpy().reshape(B, 2)
-    print(f"jc={jc}: cycles per step, sequential recursion {c[:, 0].mean() / jc:.0f}, row chain {c[:, 1].mean() / jc:.0f}")
-    a, b = o_seq.cpu().numpy()[:, :jc], o_row.cpu().numpy()[:, :jc]
-    assert np.isfinite(a[:, :, :20]).mean() > 0.5
-    assert (a[:, :, 35] == 0).any() and (a[:, :, 35] == 1).any()  # both verdicts occur
-    assert (a[:, :, :20] == 0).any()  # exact zeros occur (their signs are compared too)
-    np.testing.assert_array_equal(b.view(np.int64), a.view(np.int64))
