@@ -6,9 +6,11 @@
 // the same step -- the same operations in the same order, so the same bits -- is computed by the
 // lanes of a 16-lane row, each lane owning one COLUMN of the step's products:
 //
-//   row lane   0   1   2   3   4   5        (6..15: a dummy column, never read)
+//   row lane   0   1   2   4   5   6        (3, 7..15: a dummy column, never read)
 //   column     x0  x1  x2  s   u0  u1       s = the value function's affine part (P c + p, g)
 //
+// (the x lanes in DPP bank 0, the s and u lanes in bank 1: the u-row sums of the s and u lanes and
+// the x lanes' A^T (P B) sums accumulate into the same registers through bank-masked FMAs)
 // and every operand another lane owns arrives as the DPP row_newbcast source of a v_fmac_f64
 // (gfx950's 64-bit DPP: lane E of the row broadcast to the row inside the FMA, no separate move).
 // The value function stays where the step leaves it: lane c holds column c of P_k (rows i <= c
@@ -17,7 +19,8 @@
 //   stage 1  V_{.b} = P W_b (+ p on lane s): W_b = column b of [A c B], lane-held (9 FMAs)
 //   stage 2  Q_{ab} = H_{ab} + sum_m W_{ma} V_{mb}: W_{ma} broadcast from lane a (Hxx', Huu', gx, gu)
 //   h-seq    Hux' = H + A^T (P B) on the x lanes, from lanes u0/u1's V (the A^T (P B) order of
-//            riccati.h kAtPB, which the column lanes cannot take from stage 2 themselves)
+//            riccati.h kAtPB, which the column lanes cannot take from stage 2 themselves), into the
+//            registers that hold the u rows on the s and u lanes
 //   factor   the 2x2 L D L^T of Huu' (every lane, from three broadcasts)
 //   update   P_k = Hxx' - (r0 h0) h0^T - (r1 h1) h1^T, column c on lane c, (r h)_i from lane x_i
 // about 60 VALU instructions instead of ~128, with every row holding an instance's whole chain:
@@ -53,7 +56,8 @@ constexpr int kCols = 7;               // x0 x1 x2 s u0 u1 dummy
 // doubles per node record: 7 blocks of 8, padded to 58 so that the node lanes' records start in
 // different LDS banks (a 448-byte stride sends every fourth node lane to the same banks)
 constexpr int kRec = kBlk * kCols + 2;
-constexpr int kLX0 = 0, kLX2 = 2, kLS = 3, kLU0 = 4, kLU1 = 5;
+constexpr int kBS = 3, kBU0 = 4;        // blocks (columns) of s and u0 (x_c: block c; u1: 5)
+constexpr int kLX2 = 2, kLS = 4, kLU0 = 5, kLU1 = 6;  // lanes of x2, s, u0, u1 (x_c on lane c)
 // the value function P_j in node j's record (after its stage data are consumed): column c of P_j
 // (x0..x2; c = s: p_j) in slots [2..4] of block c
 
@@ -110,9 +114,9 @@ __device__ __forceinline__ void store_terminal(double* rk, const double* P, cons
 #pragma unroll
     for (int i = 0; i < 3; ++i) rk[c * kBlk + 2 + i] = P[symix(i, c, 3)];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) rk[kLS * kBlk + 2 + i] = p[i];
+  for (int i = 0; i < 3; ++i) rk[kBS * kBlk + 2 + i] = p[i];
 #pragma unroll
-  for (int c = kLU0; c < kCols; ++c)
+  for (int c = kBU0; c < kCols; ++c)
 #pragma unroll
     for (int i = 0; i < 3; ++i) rk[c * kBlk + 2 + i] = 0.0;
 }
@@ -125,7 +129,7 @@ __device__ __forceinline__ void load_next(const double* rk1, double* P, double* 
 #pragma unroll
     for (int i = 0; i <= c; ++i) P[symix(i, c, 3)] = rk1[c * kBlk + 2 + i];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) p[i] = rk1[kLS * kBlk + 2 + i];
+  for (int i = 0; i < 3; ++i) p[i] = rk1[kBS * kBlk + 2 + i];
 }
 
 // v_mov_b64 with a DPP row_newbcast source (the compiler sees the DPP and inserts its hazard waits)
@@ -146,7 +150,7 @@ __device__ __forceinline__ void run(const double* rec, int N) {
   // every phase of it
   int r = (int)(threadIdx.x & 15);
   asm volatile("" : "+v"(r));
-  const int col = r < 6 ? r : 6;
+  const int col = r < kLX2 + 1 ? r : (r >= kLS && r <= kLU1) ? r - 1 : 6;  // block of this lane's column
   // lane constants: the stage-1 start (P's column on lane x2, p on lane s), the unit terms of A's
   // column 2 in the orders riccati.h sums them (last on the x and s lanes, first on the u lanes),
   // A22 = 1 of the h-sequence on lane x2
@@ -154,22 +158,19 @@ __device__ __forceinline__ void run(const double* rec, int N) {
   const double m_u = (r == kLU0 || r == kLU1) ? 1.0 : 0.0;
   const double m_xs = r <= kLS ? 1.0 : 0.0;
   const double m_x2 = r == kLX2 ? 1.0 : 0.0;
-  const bool on_s = r == kLS;
   double* base = const_cast<double*>(rec) + col * kBlk;  // this lane's column block of node 0
   typedef double v2d __attribute__((ext_vector_type(2)));
   auto ld2 = [&](const double* p) __attribute__((always_inline)) { return *reinterpret_cast<const v2d*>(p); };
 
   // value function of node N (this lane's column)
   double S0 = base[N * kRec + 2], S1 = base[N * kRec + 3], S2 = base[N * kRec + 4];
-  // a step's stage data: the block's four pairs, and H(3, b), H(4, b) once more for the h-sequence's
-  // accumulators (a second LDS read instead of two register copies)
+  // a step's stage data: the block's four pairs
   struct Stage {
     v2d L0, L1, L2, L3;
-    double h3, h4;
   };
   auto load = [&](int j) __attribute__((always_inline)) {
     const double* rn = base + j * kRec;
-    return Stage{ld2(rn + 0), ld2(rn + 2), ld2(rn + 4), ld2(rn + 6), rn[3], rn[4]};
+    return Stage{ld2(rn + 0), ld2(rn + 2), ld2(rn + 4), ld2(rn + 6)};
   };
   // a step's results (into its own record, one step later)
   struct Out {
@@ -183,7 +184,7 @@ __device__ __forceinline__ void run(const double* rec, int N) {
   // wave, and a wave's LDS operations complete in order, so no wait is needed for them.
   int lw = (int)(threadIdx.x & 63) % GR;
   asm volatile("" : "+v"(lw));
-  const unsigned long long wmask = __ballot(r <= kLS && lw < 16);
+  const unsigned long long wmask = __ballot((r <= kLX2 || r == kLS) && lw < 16);
   auto store = [&](const Out& o) __attribute__((always_inline)) {
     const unsigned a = (unsigned)(unsigned long)((__attribute__((address_space(3))) double*)o.r);
     unsigned long long saved;
@@ -225,29 +226,30 @@ __device__ __forceinline__ void run(const double* rec, int N) {
         : "=&v"(V0), "=&v"(V1), "=&v"(V2)
         : "v"(S0), "v"(S1), "v"(S2), "v"(cf0), "v"(cf1), "v"(cf2), "v"(m_x2s));
     // ---- stage 2: Q_a = H_a + sum_m W_{m a} V_m (a = x0, x1, x2, u0, u1), W_{m a} from lane a --
-    // and the h-sequence: Hux'(l, c) = H(u_l, x_c) + (A^T (P B))(c, l) on lane x_c, (P B) from lane
-    // u_l (riccati.h kAtPB's order, which the column lanes cannot take from stage 2).  Three plain
-    // VALU instructions open the block (the DPP sources cf are LDS loads, V was written by stage 1)
-    double Q0, Q1, Q2, Q3 = H3, Q4 = H4, hq0 = st.h3, hq1 = st.h4;
+    // the u rows on the s and u lanes (bank 1) -- and the h-sequence on the x lanes (bank 0), into the
+    // same registers: Hux'(l, c) = H(u_l, x_c) + (A^T (P B))(c, l) on lane x_c, (P B) from lane u_l
+    // (riccati.h kAtPB's order, which the column lanes cannot take from stage 2).  Three plain VALU
+    // instructions open the block (the DPP sources cf are LDS loads, V was written by stage 1)
+    double Q0, Q1, Q2, Q3 = H3, Q4 = H4;
     asm volatile(
-        "v_add_f64 %0, %7, %10\n\t"   // Q0 = H0 + V0 (A00 = 1: column x0's only term)
-        "v_add_f64 %1, %8, %11\n\t"   // Q1 = H1 + V1
-        "v_fma_f64 %2, %12, %16, %9\n\t"  // Q2 = H2 + V2 on the u lanes (A22's unit term first there)
-        "v_fmac_f64_dpp %2, %13, %10 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"  // + A02 V0
-        "v_fmac_f64_dpp %3, %13, %10 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"  // + B00 V0
-        "v_fmac_f64_dpp %4, %13, %10 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"  // + B01 V0
-        "v_fmac_f64_dpp %2, %14, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"  // + A12 V1
-        "v_fmac_f64_dpp %3, %14, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"  // + B10 V1
-        "v_fmac_f64_dpp %4, %14, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"  // + B11 V1
-        "v_fmac_f64_dpp %4, %15, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"  // + B21 V2
-        "v_fma_f64 %2, %12, %17, %2\n\t"  // + A22 V2 last on the x and s lanes
-        "v_fmac_f64_dpp %5, %12, %18 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"  // + (PB)_20 [A22 on x2]
-        "v_fmac_f64_dpp %6, %12, %18 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %10, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"  // + (PB)_00 A0c
-        "v_fmac_f64_dpp %6, %10, %13 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %11, %14 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"  // + (PB)_10 A1c
-        "v_fmac_f64_dpp %6, %11, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf"
-        : "=&v"(Q0), "=&v"(Q1), "=&v"(Q2), "+v"(Q3), "+v"(Q4), "+v"(hq0), "+v"(hq1)
+        "v_add_f64 %0, %5, %8\n\t"   // Q0 = H0 + V0 (A00 = 1: column x0's only term)
+        "v_add_f64 %1, %6, %9\n\t"   // Q1 = H1 + V1
+        "v_fma_f64 %2, %10, %14, %7\n\t"  // Q2 = H2 + V2 on the u lanes (A22's unit term first there)
+        "v_fmac_f64_dpp %2, %11, %8 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"  // + A02 V0
+        "v_fmac_f64_dpp %3, %11, %8 row_newbcast:5 row_mask:0xf bank_mask:0x2\n\t"  // + B00 V0
+        "v_fmac_f64_dpp %4, %11, %8 row_newbcast:6 row_mask:0xf bank_mask:0x2\n\t"  // + B01 V0
+        "v_fmac_f64_dpp %2, %12, %9 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"  // + A12 V1
+        "v_fmac_f64_dpp %3, %12, %9 row_newbcast:5 row_mask:0xf bank_mask:0x2\n\t"  // + B10 V1
+        "v_fmac_f64_dpp %4, %12, %9 row_newbcast:6 row_mask:0xf bank_mask:0x2\n\t"  // + B11 V1
+        "v_fmac_f64_dpp %4, %13, %10 row_newbcast:6 row_mask:0xf bank_mask:0x2\n\t"  // + B21 V2
+        "v_fma_f64 %2, %10, %15, %2\n\t"  // + A22 V2 last on the x and s lanes
+        "v_fmac_f64_dpp %3, %10, %16 row_newbcast:5 row_mask:0xf bank_mask:0x1\n\t"  // + (PB)_20 [A22 on x2]
+        "v_fmac_f64_dpp %4, %10, %16 row_newbcast:6 row_mask:0xf bank_mask:0x1\n\t"
+        "v_fmac_f64_dpp %3, %8, %11 row_newbcast:5 row_mask:0xf bank_mask:0x1\n\t"  // + (PB)_00 A0c
+        "v_fmac_f64_dpp %4, %8, %11 row_newbcast:6 row_mask:0xf bank_mask:0x1\n\t"
+        "v_fmac_f64_dpp %3, %9, %12 row_newbcast:5 row_mask:0xf bank_mask:0x1\n\t"  // + (PB)_10 A1c
+        "v_fmac_f64_dpp %4, %9, %12 row_newbcast:6 row_mask:0xf bank_mask:0x1"
+        : "=&v"(Q0), "=&v"(Q1), "=&v"(Q2), "+v"(Q3), "+v"(Q4)
         : "v"(H0), "v"(H1), "v"(H2), "v"(V0), "v"(V1), "v"(V2), "v"(cf0), "v"(cf1), "v"(cf2), "v"(m_u),
           "v"(m_xs), "v"(m_x2));
     // the stage data are consumed: the next step's (record j - 1; at j = 0 a harmless re-read of
@@ -261,9 +263,8 @@ __device__ __forceinline__ void run(const double* rec, int N) {
     if (!(MPCX_ROWCHAIN_PROBE & 2)) nx = load(j > 0 ? j - 1 : 0);
     else nx = st;
     __builtin_amdgcn_sched_barrier(0);
-    // lane s: g0 = gu0, and gu1 for g1 (stage 2's u0 / u1 sums there)
-    const double h0c = on_s ? Q3 : hq0;
-    const double hu1c = on_s ? Q4 : hq1;
+    // lane x_c: Hux'(0, c), Hux'(1, c); lane s: gu0 (g0) and gu1 for g1 (stage 2's u rows there)
+    const double h0c = Q3, hu1c = Q4;
     // ---- factor: Huu' = [[a, b], [b, d]] (a on lane u0, b and d on lane u1), every lane
     const double fa = bcast<kLU0>(Q3), fb = bcast<kLU1>(Q3), fd = bcast<kLU1>(Q4);
     const double det = fma(fa, fd, -fb * fb);
