@@ -45,8 +45,7 @@ namespace mpcx {
 namespace rowchain {
 
 // diagnostic switches of tools/rowchain_probe.py (timing of the chain's parts in the test harness only;
-// 0 in every product build): 1 = no value-function stores, 2 = no stage loads after the first,
-// 4 = no reciprocals
+// 0 in every product build): 1 = no value-function stores, 2 = no stage loads after the first
 #ifndef MPCX_ROWCHAIN_PROBE
 #define MPCX_ROWCHAIN_PROBE 0
 #endif
@@ -225,52 +224,66 @@ __device__ __forceinline__ void run(const double* rec, int N) {
         "v_fmac_f64_dpp %2, %5, %8 row_newbcast:2 row_mask:0xf bank_mask:0xf"      // V2 += P22 w2
         : "=&v"(V0), "=&v"(V1), "=&v"(V2)
         : "v"(S0), "v"(S1), "v"(S2), "v"(cf0), "v"(cf1), "v"(cf2), "v"(m_x2s));
-    // ---- stage 2: Q_a = H_a + sum_m W_{m a} V_m (a = x0, x1, x2, u0, u1), W_{m a} from lane a --
-    // the u rows on the s and u lanes (bank 1) -- and the h-sequence on the x lanes (bank 0), into the
-    // same registers: Hux'(l, c) = H(u_l, x_c) + (A^T (P B))(c, l) on lane x_c, (P B) from lane u_l
-    // (riccati.h kAtPB's order, which the column lanes cannot take from stage 2).  Three plain VALU
-    // instructions open the block (the DPP sources cf are LDS loads, V was written by stage 1)
-    double Q0, Q1, Q2, Q3 = H3, Q4 = H4;
-    asm volatile(
-        "v_add_f64 %0, %5, %8\n\t"   // Q0 = H0 + V0 (A00 = 1: column x0's only term)
-        "v_add_f64 %1, %6, %9\n\t"   // Q1 = H1 + V1
-        "v_fma_f64 %2, %10, %14, %7\n\t"  // Q2 = H2 + V2 on the u lanes (A22's unit term first there)
-        "v_fmac_f64_dpp %2, %11, %8 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"  // + A02 V0
-        "v_fmac_f64_dpp %3, %11, %8 row_newbcast:5 row_mask:0xf bank_mask:0x2\n\t"  // + B00 V0
-        "v_fmac_f64_dpp %4, %11, %8 row_newbcast:6 row_mask:0xf bank_mask:0x2\n\t"  // + B01 V0
-        "v_fmac_f64_dpp %2, %12, %9 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"  // + A12 V1
-        "v_fmac_f64_dpp %3, %12, %9 row_newbcast:5 row_mask:0xf bank_mask:0x2\n\t"  // + B10 V1
-        "v_fmac_f64_dpp %4, %12, %9 row_newbcast:6 row_mask:0xf bank_mask:0x2\n\t"  // + B11 V1
-        "v_fmac_f64_dpp %4, %13, %10 row_newbcast:6 row_mask:0xf bank_mask:0x2\n\t"  // + B21 V2
-        "v_fma_f64 %2, %10, %15, %2\n\t"  // + A22 V2 last on the x and s lanes
-        "v_fmac_f64_dpp %3, %10, %16 row_newbcast:5 row_mask:0xf bank_mask:0x1\n\t"  // + (PB)_20 [A22 on x2]
-        "v_fmac_f64_dpp %4, %10, %16 row_newbcast:6 row_mask:0xf bank_mask:0x1\n\t"
-        "v_fmac_f64_dpp %3, %8, %11 row_newbcast:5 row_mask:0xf bank_mask:0x1\n\t"  // + (PB)_00 A0c
-        "v_fmac_f64_dpp %4, %8, %11 row_newbcast:6 row_mask:0xf bank_mask:0x1\n\t"
-        "v_fmac_f64_dpp %3, %9, %12 row_newbcast:5 row_mask:0xf bank_mask:0x1\n\t"  // + (PB)_10 A1c
-        "v_fmac_f64_dpp %4, %9, %12 row_newbcast:6 row_mask:0xf bank_mask:0x1"
-        : "=&v"(Q0), "=&v"(Q1), "=&v"(Q2), "+v"(Q3), "+v"(Q4)
-        : "v"(H0), "v"(H1), "v"(H2), "v"(V0), "v"(V1), "v"(V2), "v"(cf0), "v"(cf1), "v"(cf2), "v"(m_u),
-          "v"(m_xs), "v"(m_x2));
-    // the stage data are consumed: the next step's (record j - 1; at j = 0 a harmless re-read of
-    // record 0) load into the same registers behind the factor and the update, which hide their
-    // latency
+    // the stage data are being consumed; the next step's record (j - 1; at j = 0 a harmless re-read of
+    // record 0) loads into the other register set while this step runs, and the previous step's
+    // results go out first (LDS operations complete in order, so the next step's wait covers them)
     __builtin_amdgcn_sched_barrier(0);
-    // the previous step's results go out first: behind this step's stage 2, well before the next
-    // step waits for its loads (LDS operations complete in order, so that wait covers the stores too)
     if constexpr (decltype(prev)::value)
       if (!(MPCX_ROWCHAIN_PROBE & 1)) store(po);
     if (!(MPCX_ROWCHAIN_PROBE & 2)) nx = load(j > 0 ? j - 1 : 0);
     else nx = st;
     __builtin_amdgcn_sched_barrier(0);
+    // ---- stage 2 and the factor in one block, so that the x rows fill the reciprocals' latency.
+    // Stage 2: Q_a = H_a + sum_m W_{m a} V_m (a = x0, x1, x2, u0, u1), W_{m a} from lane a -- the u
+    // rows on the s and u lanes (bank 1) -- and the h-sequence on the x lanes (bank 0), into the same
+    // registers: Hux'(l, c) = H(u_l, x_c) + (A^T (P B))(c, l) on lane x_c, (P B) from lane u_l
+    // (riccati.h kAtPB's order, which the column lanes cannot take from stage 2).  Factor: Huu' =
+    // [[a, b], [b, d]] (a on lane u0, b and d on lane u1) on every lane, det = a d - b^2, r0 = 1/a and
+    // 1/det as rcp64 (v_rcp_f64 and two Newton steps), t = b r0, r1 = a / det -- riccati.h's operations
+    // in its order.  The DPP sources are LDS loads, V (stage 1, at least ten instructions back) and Q3 /
+    // Q4 (last written three and four instructions before their broadcasts)
+    double Q0, Q1, Q2, Q3 = H3, Q4 = H4, r0, t, r1, fa, fb, fd, det, rdet, e0, e1;
+    asm volatile(
+        "v_fmac_f64_dpp %3, %21, %18 row_newbcast:5 row_mask:0xf bank_mask:0x2\n\t"  // Q3 + B00 V0
+        "v_fmac_f64_dpp %4, %21, %18 row_newbcast:6 row_mask:0xf bank_mask:0x2\n\t"  // Q4 + B01 V0
+        "v_fmac_f64_dpp %3, %22, %19 row_newbcast:5 row_mask:0xf bank_mask:0x2\n\t"  // + B10 V1
+        "v_fmac_f64_dpp %4, %22, %19 row_newbcast:6 row_mask:0xf bank_mask:0x2\n\t"  // + B11 V1
+        "v_fmac_f64_dpp %4, %23, %20 row_newbcast:6 row_mask:0xf bank_mask:0x2\n\t"  // + B21 V2
+        "v_fmac_f64_dpp %3, %20, %26 row_newbcast:5 row_mask:0xf bank_mask:0x1\n\t"  // + (PB)_20 [A22 on x2]
+        "v_fmac_f64_dpp %4, %20, %26 row_newbcast:6 row_mask:0xf bank_mask:0x1\n\t"
+        "v_fmac_f64_dpp %3, %18, %21 row_newbcast:5 row_mask:0xf bank_mask:0x1\n\t"  // + (PB)_00 A0c
+        "v_fmac_f64_dpp %4, %18, %21 row_newbcast:6 row_mask:0xf bank_mask:0x1\n\t"
+        "v_fmac_f64_dpp %3, %19, %22 row_newbcast:5 row_mask:0xf bank_mask:0x1\n\t"  // + (PB)_10 A1c
+        "v_fmac_f64_dpp %4, %19, %22 row_newbcast:6 row_mask:0xf bank_mask:0x1\n\t"
+        "v_add_f64 %0, %15, %18\n\t"          // Q0 = H0 + V0 (A00 = 1: column x0's only term)
+        "v_add_f64 %1, %16, %19\n\t"          // Q1 = H1 + V1
+        "v_mov_b64_dpp %8, %3 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"   // a
+        "v_mov_b64_dpp %9, %3 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"   // b
+        "v_mov_b64_dpp %10, %4 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"  // d
+        "v_rcp_f64 %5, %8\n\t"                // r0 ~ 1/a
+        "v_mul_f64 %11, %9, -%9\n\t"          // det = -b b
+        "v_fmac_f64 %11, %8, %10\n\t"         //       + a d
+        "v_fma_f64 %2, %20, %24, %17\n\t"     // Q2 = H2 + V2 on the u lanes (A22's unit term first there)
+        "v_rcp_f64 %12, %11\n\t"              // rdet ~ 1/det
+        "v_fma_f64 %13, -%8, %5, 1.0\n\t"
+        "v_fmac_f64_dpp %2, %21, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"  // + A02 V0
+        "v_fmac_f64 %5, %5, %13\n\t"
+        "v_fma_f64 %14, -%11, %12, 1.0\n\t"
+        "v_fmac_f64_dpp %2, %22, %19 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"  // + A12 V1
+        "v_fma_f64 %13, -%8, %5, 1.0\n\t"
+        "v_fmac_f64 %12, %12, %14\n\t"
+        "v_fma_f64 %2, %20, %25, %2\n\t"      // + A22 V2 last on the x and s lanes
+        "v_fmac_f64 %5, %5, %13\n\t"          // r0
+        "v_fma_f64 %14, -%11, %12, 1.0\n\t"
+        "v_mul_f64 %6, %9, %5\n\t"            // t = b r0
+        "v_fmac_f64 %12, %12, %14\n\t"        // rdet
+        "v_mul_f64 %7, %8, %12"               // r1 = a rdet
+        : "=&v"(Q0), "=&v"(Q1), "=&v"(Q2), "+v"(Q3), "+v"(Q4), "=&v"(r0), "=&v"(t), "=&v"(r1), "=&v"(fa),
+          "=&v"(fb), "=&v"(fd), "=&v"(det), "=&v"(rdet), "=&v"(e0), "=&v"(e1)
+        : "v"(H0), "v"(H1), "v"(H2), "v"(V0), "v"(V1), "v"(V2), "v"(cf0), "v"(cf1), "v"(cf2), "v"(m_u),
+          "v"(m_xs), "v"(m_x2));
     // lane x_c: Hux'(0, c), Hux'(1, c); lane s: gu0 (g0) and gu1 for g1 (stage 2's u rows there)
     const double h0c = Q3, hu1c = Q4;
-    // ---- factor: Huu' = [[a, b], [b, d]] (a on lane u0, b and d on lane u1), every lane
-    const double fa = bcast<kLU0>(Q3), fb = bcast<kLU1>(Q3), fd = bcast<kLU1>(Q4);
-    const double det = fma(fa, fd, -fb * fb);
-    const double r0 = (MPCX_ROWCHAIN_PROBE & 4) ? fa : rcp64(fa), rdet = (MPCX_ROWCHAIN_PROBE & 4) ? det : rcp64(det);
-    const double t = fb * r0;
-    const double r1 = fa * rdet;
     // ---- update: P_k(i, c) = Hxx'(i, c) - (r0 h0_i) h0_c - (r1 h1_i) h1_c, (r h)_i from lane x_i.
     // R0 is written two VALU instructions before its first DPP read, R1 three: no s_nop
     double R0, R1, h1c;
