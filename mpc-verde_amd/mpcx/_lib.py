@@ -85,8 +85,8 @@ def _bind_single_hip_runtime():
 
 def source_hash():
     """Hash of the library's sources in the tree, computed as mpc-verde_amd/Makefile does
-    (the sorted csrc/*.hip, csrc/capi.cpp, the sorted csrc/*.h, then include/mpcx.h; sha256,
-    16 hex digits), or None
+    (the sorted csrc/*.hip, csrc/capi.cpp, the sorted csrc/*.h, include/mpcx.h, then the Makefile
+    for its compiler flags; sha256, 16 hex digits), or None
     when the sources are not next to the package (an installed copy)."""
     import glob
     import hashlib
@@ -96,6 +96,7 @@ def source_hash():
     files.append(os.path.join(pkg, "csrc", "capi.cpp"))
     files += sorted(glob.glob(os.path.join(pkg, "csrc", "*.h")))
     files.append(os.path.join(os.path.dirname(pkg), "include", "mpcx.h"))
+    files.append(os.path.join(pkg, "Makefile"))
     if not all(os.path.exists(f) for f in files):
         return None
     h = hashlib.sha256()
