@@ -7,7 +7,7 @@
 set -euo pipefail
 TAG=$1; UNIT=$2; shift 2
 cd "$(dirname "$0")/../mpc-verde_amd"
-HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -mllvm -disable-machine-licm"  # as the Makefile (DEVFLAGS)
+HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -mllvm -disable-machine-licm -mllvm -sink-insts-to-avoid-spills"  # as the Makefile (DEVFLAGS)
 mkdir -p build/exp_$TAG
 /opt/rocm/bin/hipcc $HIPFLAGS -I../include -Icsrc "$@" -c csrc/solve_$UNIT.hip -o build/exp_$TAG/solve_$UNIT.hip.o
 BASE=${EXP_BASE:-build}  # build/stamps: link with the diagnostic build's objects
