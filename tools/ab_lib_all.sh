@@ -5,7 +5,7 @@
 #   tools/ab_lib_all.sh "LIB_A LIB_B ..." [reps] [workloads: c2 c3 c4 c5 kin dyn cp]
 set -o pipefail
 LIBS=($1); R=${2:-2}; W=${3:-"c2 c3 c4 c5 kin dyn cp"}
-name() { basename "$(dirname "$(dirname "$(dirname "$1")")")"; }
+name() { case "$1" in */mpc-verde_amd/mpcx/libmpcx.so) basename "$(dirname "$(dirname "$(dirname "$1")")")" ;; *) basename "$1" .so ;; esac; }
 for w in c2 c5 dyn; do
   for L in "${LIBS[@]}"; do
     MPCX_LIB=$L MPCX_ALLOW_STALE_LIB=1 timeout -k 10 200 python3 tools/bits_compare.py $w /tmp/ab_bits_${w}_$(name $L).npz > /dev/null 2>&1 || exit 1
